@@ -1,0 +1,516 @@
+// hector_capi.hip -- host runtime + extern "C" boundary (include/slam2d/hector.h) for the MI355X
+// Hector path.  Mirrors HectorSlamProcessor / MapRepMultiMap (lesson4/include/lesson4/hector_mapping/
+// slam_main/) over device-resident state; every compute step is a HIP kernel (hector_kernels.hip).
+// There is no CPU fallback: without a usable HIP device hs_create fails with HS_ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/slam2d/hector.h"
+#include "hector_kernels.hip"
+
+using namespace s2d;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char *what, hipError_t e = hipSuccess)
+{
+    g_err = what;
+    if (e != hipSuccess) {
+        g_err += ": ";
+        g_err += hipGetErrorString(e);
+    }
+    return code;
+}
+
+#define HCHK(expr)                                          \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return fail(HS_EHIP, #expr, _e); \
+    } while (0)
+
+constexpr int NKERN = 4;
+
+struct EventPair {
+    hipEvent_t a, b;
+    int kernel;
+};
+}  // namespace
+
+struct hs_ctx {
+    int B = 0, levels = 0, max_points = 0, sx = 0, sy = 0;
+    float res = 0, start_x = 0, start_y = 0;
+    FleetGeom geom{};
+    LogOddsCell *d_cells = nullptr;
+    size_t cells_bytes = 0;
+    StreamState *d_state = nullptr;
+    // single-stream staging (host-pointer entry points)
+    float2 *d_pts1 = nullptr;
+    int *d_n1 = nullptr;
+    float2 *d_origo1 = nullptr;
+    float *d_hint1 = nullptr;
+    float *d_out_pose = nullptr;
+    float *d_out_cov = nullptr;
+    int8_t *d_occ = nullptr;
+    hipStream_t stream = nullptr;
+    // timing
+    bool timing = false;
+    std::vector<EventPair> ev_used, ev_free;
+    double acc_ms[NKERN] = {0, 0, 0, 0};
+    int64_t acc_n[NKERN] = {0, 0, 0, 0};
+};
+
+namespace {
+
+// MapRepMultiMap ctor (MapRepMultiMap.h:57-90) + GridMapBase::setMapTransformation (GridMapBase.h:270-286)
+void init_geometry(hs_ctx *c)
+{
+    FleetGeom &g = c->geom;
+    g.levels = c->levels;
+    int rx = c->sx, ry = c->sy;
+    float res = c->res;
+    float total_x = c->res * (float)c->sx;
+    float mid_x = total_x * c->start_x;
+    float total_y = c->res * (float)c->sy;
+    float mid_y = total_y * c->start_y;
+    size_t off = 0;
+    for (int i = 0; i < c->levels; ++i) {
+        LevelGeom &L = g.lv[i];
+        L.sx = rx;
+        L.sy = ry;
+        L.lim[0] = (float)rx - 2.0f;
+        L.lim[1] = (float)ry - 2.0f;
+        L.cell_len = res;
+        L.scale = 1.0f / res;
+        L.map_t[0] = L.scale * mid_x;
+        L.map_t[1] = L.scale * mid_y;
+        float m00 = L.scale, m01 = 0.0f, m10 = 0.0f, m11 = L.scale;
+        float det = m00 * m11 - m10 * m01;
+        float invdet = 1.0f / det;
+        L.inv_l[0] = m11 * invdet;
+        L.inv_l[2] = -m10 * invdet;
+        L.inv_l[1] = -m01 * invdet;
+        L.inv_l[3] = m00 * invdet;
+        L.inv_t[0] = (-L.inv_l[0]) * L.map_t[0] + (-L.inv_l[1]) * L.map_t[1];
+        L.inv_t[1] = (-L.inv_l[2]) * L.map_t[0] + (-L.inv_l[3]) * L.map_t[1];
+        L.pts_scale = (float)(1.0 / pow(2.0, (double)i));
+        L.cell_offset = off;
+        off += (size_t)rx * (size_t)ry;
+        rx /= 2;
+        ry /= 2;
+        res *= 2.0f;
+    }
+    g.stream_cells = off;
+}
+
+// GridMapLogOddsFunctions::probToLogOdds  GridMapLogOdds.h:153-157
+float prob_to_logodds(float prob)
+{
+    float odds = prob / (1.0f - prob);
+    return (float)log((double)odds);
+}
+
+StreamState initial_state()
+{
+    // HectorSlamProcessor::reset (HectorSlamProcessor.h:111-117); OccGridMapBase ctor indices
+    StreamState st;
+    memset(&st, 0, sizeof(st));
+    st.last_upd_pose[0] = st.last_upd_pose[1] = st.last_upd_pose[2] = FLT_MAX;
+    st.cur_update_index = 0;
+    st.map_updates = 0;
+    return st;
+}
+
+int reset_all(hs_ctx *c)
+{
+    size_t ncell = c->cells_bytes / sizeof(LogOddsCell);
+    hipLaunchKernelGGL(hs_fill_cells_kernel, dim3(4096), dim3(256), 0, c->stream, c->d_cells, ncell);
+    HCHK(hipGetLastError());
+    std::vector<StreamState> h(c->B, initial_state());
+    HCHK(hipMemcpyAsync(c->d_state, h.data(), sizeof(StreamState) * c->B, hipMemcpyHostToDevice, c->stream));
+    HCHK(hipStreamSynchronize(c->stream));
+    return HS_OK;
+}
+
+EventPair *begin_timed(hs_ctx *c, int kernel, hipStream_t s)
+{
+    if (!c->timing) return nullptr;
+    EventPair p;
+    if (!c->ev_free.empty()) {
+        p = c->ev_free.back();
+        c->ev_free.pop_back();
+    } else {
+        if (hipEventCreate(&p.a) != hipSuccess || hipEventCreate(&p.b) != hipSuccess) return nullptr;
+    }
+    p.kernel = kernel;
+    hipEventRecord(p.a, s);
+    c->ev_used.push_back(p);
+    return &c->ev_used.back();
+}
+
+void end_timed(hs_ctx *c, hipStream_t s)
+{
+    if (!c->timing || c->ev_used.empty()) return;
+    hipEventRecord(c->ev_used.back().b, s);
+}
+
+int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride, const int *n, const float2 *origo,
+                const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s)
+{
+    if (count <= 0) return HS_OK;
+    begin_timed(c, 0, s);
+    hipLaunchKernelGGL(hs_match_kernel, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state, xy,
+                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov);
+    end_timed(c, s);
+    HCHK(hipGetLastError());
+    if (mode == MODE_MATCH_ONLY) return HS_OK;
+    const int nb256 = (c->max_points + 255) / 256;
+    const int nb64 = (c->max_points + FREE_BEAMS - 1) / FREE_BEAMS;
+    begin_timed(c, 1, s);
+    hipLaunchKernelGGL(hs_mark_hits_kernel, dim3(nb256, c->levels, count), dim3(256), 0, s, c->geom, c->d_cells,
+                       c->d_state, xy, xy_stride, begin);
+    end_timed(c, s);
+    HCHK(hipGetLastError());
+    begin_timed(c, 2, s);
+    hipLaunchKernelGGL(hs_free_cells_kernel, dim3(nb64, c->levels, count), dim3(256), 0, s, c->geom, c->d_cells,
+                       c->d_state, xy, xy_stride, begin);
+    end_timed(c, s);
+    HCHK(hipGetLastError());
+    begin_timed(c, 3, s);
+    hipLaunchKernelGGL(hs_resolve_hits_kernel, dim3(nb256, c->levels, count), dim3(256), 0, s, c->geom, c->d_cells,
+                       c->d_state, xy, xy_stride, begin);
+    end_timed(c, s);
+    HCHK(hipGetLastError());
+    return HS_OK;
+}
+
+int check_stream(hs_ctx *c, int stream) { return (c && stream >= 0 && stream < c->B) ? HS_OK : HS_EINVAL; }
+
+// Stage one host scan into the single-stream buffers.
+int stage_scan(hs_ctx *c, const float *xy, int n, float ox, float oy, const float *hint)
+{
+    if (n < 0 || n > c->max_points || (n > 0 && !xy)) return fail(HS_EINVAL, "bad scan size / pointer");
+    if (n > 0) HCHK(hipMemcpyAsync(c->d_pts1, xy, sizeof(float2) * n, hipMemcpyHostToDevice, c->stream));
+    HCHK(hipMemcpyAsync(c->d_n1, &n, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    float2 o = make_float2(ox, oy);
+    HCHK(hipMemcpyAsync(c->d_origo1, &o, sizeof(float2), hipMemcpyHostToDevice, c->stream));
+    if (hint) HCHK(hipMemcpyAsync(c->d_hint1, hint, sizeof(float) * 3, hipMemcpyHostToDevice, c->stream));
+    return HS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *hs_version(void) { return "slam2d-mi355x hector 0.1 (gfx950)"; }
+const char *hs_last_error(void) { return g_err.c_str(); }
+
+int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_x, int map_size_y, float map_start_x,
+              float map_start_y, int levels, int max_points)
+{
+    if (!out) return fail(HS_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (num_streams < 1 || levels < 1 || levels > HS_MAX_LEVELS || map_size_x < 2 || map_size_y < 2 ||
+        max_points < 1 || !(map_resolution > 0.0f))
+        return fail(HS_EINVAL, "invalid hs_create arguments");
+    if ((map_size_x >> (levels - 1)) < 2 || (map_size_y >> (levels - 1)) < 2)
+        return fail(HS_EINVAL, "map too small for the requested number of levels");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(HS_ENODEV, "no HIP device");
+    hs_ctx *c = new hs_ctx();
+    c->B = num_streams;
+    c->levels = levels;
+    c->max_points = max_points;
+    c->sx = map_size_x;
+    c->sy = map_size_y;
+    c->res = map_resolution;
+    c->start_x = map_start_x;
+    c->start_y = map_start_y;
+    init_geometry(c);
+    c->geom.lf = prob_to_logodds(0.4f);  // GridMapLogOddsFunctions ctor (GridMapLogOdds.h:98-102)
+    c->geom.lo = prob_to_logodds(0.6f);
+    c->geom.min_dist = 0.4f * 1.0f;      // HectorSlamProcessor ctor (HectorSlamProcessor.h:66-67)
+    c->geom.min_ang = 0.13f * 1.0f;
+    c->cells_bytes = sizeof(LogOddsCell) * c->geom.stream_cells * (size_t)num_streams;
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+        delete c;
+        return fail(HS_EHIP, "hipStreamCreate", e);
+    }
+    if ((e = hipMalloc(&c->d_cells, c->cells_bytes)) != hipSuccess ||
+        (e = hipMalloc(&c->d_state, sizeof(StreamState) * num_streams)) != hipSuccess ||
+        (e = hipMalloc(&c->d_pts1, sizeof(float2) * max_points)) != hipSuccess ||
+        (e = hipMalloc(&c->d_n1, sizeof(int))) != hipSuccess ||
+        (e = hipMalloc(&c->d_origo1, sizeof(float2))) != hipSuccess ||
+        (e = hipMalloc(&c->d_hint1, sizeof(float) * 3)) != hipSuccess ||
+        (e = hipMalloc(&c->d_out_pose, sizeof(float) * 3 * num_streams)) != hipSuccess ||
+        (e = hipMalloc(&c->d_out_cov, sizeof(float) * 9 * num_streams)) != hipSuccess ||
+        (e = hipMalloc(&c->d_occ, (size_t)map_size_x * map_size_y)) != hipSuccess) {
+        hs_destroy(c);
+        return fail(HS_ENOMEM, "hipMalloc", e);
+    }
+    int rc = reset_all(c);
+    if (rc != HS_OK) {
+        hs_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return HS_OK;
+}
+
+int hs_destroy(hs_ctx *c)
+{
+    if (!c) return HS_OK;
+    if (c->stream) hipStreamSynchronize(c->stream);
+    hipFree(c->d_cells);
+    hipFree(c->d_state);
+    hipFree(c->d_pts1);
+    hipFree(c->d_n1);
+    hipFree(c->d_origo1);
+    hipFree(c->d_hint1);
+    hipFree(c->d_out_pose);
+    hipFree(c->d_out_cov);
+    hipFree(c->d_occ);
+    for (auto &p : c->ev_used) {
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    for (auto &p : c->ev_free) {
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return HS_OK;
+}
+
+int hs_reset(hs_ctx *c)
+{
+    if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    return reset_all(c);
+}
+
+int hs_set_update_factors(hs_ctx *c, float free_factor, float occupied_factor)
+{
+    if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    c->geom.lf = prob_to_logodds(free_factor);
+    c->geom.lo = prob_to_logodds(occupied_factor);
+    return HS_OK;
+}
+
+int hs_set_map_update_thresholds(hs_ctx *c, float min_dist, float min_angle)
+{
+    if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    c->geom.min_dist = min_dist;
+    c->geom.min_ang = min_angle;
+    return HS_OK;
+}
+
+int hs_get_scale_to_map(hs_ctx *c, float *scale_out)
+{
+    if (!c || !scale_out) return fail(HS_EINVAL, "NULL argument");
+    *scale_out = c->geom.lv[0].scale;
+    return HS_OK;
+}
+
+int hs_get_map_levels(hs_ctx *c, int *levels_out)
+{
+    if (!c || !levels_out) return fail(HS_EINVAL, "NULL argument");
+    *levels_out = c->levels;
+    return HS_OK;
+}
+
+int hs_get_map_info(hs_ctx *c, int level, int *size_x, int *size_y, float *cell_length, float *origin_xy)
+{
+    if (!c || level < 0 || level >= c->levels) return fail(HS_EINVAL, "bad level");
+    const LevelGeom &L = c->geom.lv[level];
+    if (size_x) *size_x = L.sx;
+    if (size_y) *size_y = L.sy;
+    if (cell_length) *cell_length = L.cell_len;
+    if (origin_xy) {
+        // getWorldCoords(0,0) (hector_slam.cc:167)
+        origin_xy[0] = L.inv_t[0] + (L.inv_l[0] * 0.0f + L.inv_l[1] * 0.0f);
+        origin_xy[1] = L.inv_t[1] + (L.inv_l[2] * 0.0f + L.inv_l[3] * 0.0f);
+    }
+    return HS_OK;
+}
+
+int hs_update(hs_ctx *c, int stream, const float *xy, int n, float ox, float oy, const float *hint,
+              int map_without_matching, float pose_out[3], float cov_out[9], int *did_update_out)
+{
+    if (check_stream(c, stream) != HS_OK) return fail(HS_EINVAL, "bad ctx/stream");
+    int rc = stage_scan(c, xy, n, ox, oy, hint);
+    if (rc != HS_OK) return rc;
+    rc = launch_step(c, stream, 1, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, hint ? c->d_hint1 : nullptr,
+                     map_without_matching ? MODE_NO_MATCH_FORCE : MODE_PROCESS, c->d_out_pose, c->d_out_cov, c->stream);
+    if (rc != HS_OK) return rc;
+    StreamState st;
+    HCHK(hipMemcpyAsync(&st, c->d_state + stream, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+    HCHK(hipStreamSynchronize(c->stream));
+    if (pose_out) memcpy(pose_out, st.pose, sizeof(float) * 3);
+    if (cov_out) memcpy(cov_out, st.cov, sizeof(float) * 9);
+    if (did_update_out) *did_update_out = st.do_update;
+    return HS_OK;
+}
+
+int hs_match(hs_ctx *c, int stream, const float *xy, int n, float ox, float oy, const float hint[3], float pose_out[3],
+             float cov_out[9])
+{
+    if (check_stream(c, stream) != HS_OK || !hint) return fail(HS_EINVAL, "bad ctx/stream/hint");
+    int rc = stage_scan(c, xy, n, ox, oy, hint);
+    if (rc != HS_OK) return rc;
+    rc = launch_step(c, stream, 1, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, c->d_hint1, MODE_MATCH_ONLY,
+                     c->d_out_pose, c->d_out_cov, c->stream);
+    if (rc != HS_OK) return rc;
+    float p[3], cv[9];
+    HCHK(hipMemcpyAsync(p, c->d_out_pose, sizeof(p), hipMemcpyDeviceToHost, c->stream));
+    HCHK(hipMemcpyAsync(cv, c->d_out_cov, sizeof(cv), hipMemcpyDeviceToHost, c->stream));
+    HCHK(hipStreamSynchronize(c->stream));
+    if (pose_out) memcpy(pose_out, p, sizeof(p));
+    if (cov_out) memcpy(cov_out, cv, sizeof(cv));
+    return HS_OK;
+}
+
+int hs_update_by_scan(hs_ctx *c, int stream, const float *xy, int n, float ox, float oy, const float pose[3])
+{
+    if (check_stream(c, stream) != HS_OK || !pose) return fail(HS_EINVAL, "bad ctx/stream/pose");
+    int rc = stage_scan(c, xy, n, ox, oy, pose);
+    if (rc != HS_OK) return rc;
+    rc = launch_step(c, stream, 1, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, c->d_hint1, MODE_UPDATE_ONLY,
+                     nullptr, nullptr, c->stream);
+    if (rc != HS_OK) return rc;
+    HCHK(hipStreamSynchronize(c->stream));
+    return HS_OK;
+}
+
+int hs_get_last_pose(hs_ctx *c, int stream, float pose_out[3], float cov_out[9])
+{
+    if (check_stream(c, stream) != HS_OK) return fail(HS_EINVAL, "bad ctx/stream");
+    StreamState st;
+    HCHK(hipMemcpyAsync(&st, c->d_state + stream, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+    HCHK(hipStreamSynchronize(c->stream));
+    if (pose_out) memcpy(pose_out, st.pose, sizeof(float) * 3);
+    if (cov_out) memcpy(cov_out, st.cov, sizeof(float) * 9);
+    return HS_OK;
+}
+
+int hs_get_map(hs_ctx *c, int stream, int level, int8_t *occ_out, float *logodds_out, int32_t *upd_out,
+               int *update_index_out)
+{
+    if (check_stream(c, stream) != HS_OK || level < 0 || level >= c->levels) return fail(HS_EINVAL, "bad stream/level");
+    const LevelGeom &L = c->geom.lv[level];
+    const size_t ncell = (size_t)L.sx * L.sy;
+    const LogOddsCell *base = c->d_cells + (size_t)stream * c->geom.stream_cells + L.cell_offset;
+    if (occ_out) {
+        hipLaunchKernelGGL(hs_publish_kernel, dim3(1024), dim3(256), 0, c->stream, base, c->d_occ, ncell);
+        HCHK(hipGetLastError());
+        HCHK(hipMemcpyAsync(occ_out, c->d_occ, ncell, hipMemcpyDeviceToHost, c->stream));
+    }
+    std::vector<LogOddsCell> tmp;
+    if (logodds_out || upd_out) {
+        tmp.resize(ncell);
+        HCHK(hipMemcpyAsync(tmp.data(), base, sizeof(LogOddsCell) * ncell, hipMemcpyDeviceToHost, c->stream));
+    }
+    StreamState st;
+    HCHK(hipMemcpyAsync(&st, c->d_state + stream, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+    HCHK(hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i < tmp.size(); ++i) {
+        if (logodds_out) logodds_out[i] = tmp[i].l;
+        if (upd_out) upd_out[i] = tmp[i].upd;
+    }
+    if (update_index_out) *update_index_out = st.map_updates - 1;
+    return HS_OK;
+}
+
+int hs_set_map(hs_ctx *c, int stream, int level, const float *logodds, const int32_t *upd)
+{
+    if (check_stream(c, stream) != HS_OK || level < 0 || level >= c->levels || !logodds || !upd)
+        return fail(HS_EINVAL, "bad arguments");
+    const LevelGeom &L = c->geom.lv[level];
+    const size_t ncell = (size_t)L.sx * L.sy;
+    std::vector<LogOddsCell> tmp(ncell);
+    for (size_t i = 0; i < ncell; ++i) {
+        tmp[i].l = logodds[i];
+        tmp[i].upd = upd[i];
+    }
+    LogOddsCell *base = c->d_cells + (size_t)stream * c->geom.stream_cells + L.cell_offset;
+    HCHK(hipMemcpyAsync(base, tmp.data(), sizeof(LogOddsCell) * ncell, hipMemcpyHostToDevice, c->stream));
+    HCHK(hipStreamSynchronize(c->stream));
+    return HS_OK;
+}
+
+int hs_step_batch_device(hs_ctx *c, int stream_begin, int count, const float *d_xy, int xy_stride, const int *d_n,
+                         const float *d_origo, const float *d_hints, void *hip_stream)
+{
+    if (!c || stream_begin < 0 || count < 0 || stream_begin + count > c->B || !d_xy || !d_n ||
+        xy_stride < c->max_points)
+        return fail(HS_EINVAL, "bad batch arguments (xy_stride must be >= max_points)");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    return launch_step(c, stream_begin, count, (const float2 *)d_xy, xy_stride, d_n, (const float2 *)d_origo, d_hints,
+                       MODE_PROCESS, nullptr, nullptr, s);
+}
+
+int hs_get_poses(hs_ctx *c, float *poses_out, float *covs_out, int *did_update_out, int64_t *cells_out)
+{
+    if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    std::vector<StreamState> h(c->B);
+    HCHK(hipDeviceSynchronize());
+    HCHK(hipMemcpy(h.data(), c->d_state, sizeof(StreamState) * c->B, hipMemcpyDeviceToHost));
+    for (int s = 0; s < c->B; ++s) {
+        if (poses_out) memcpy(poses_out + 3 * s, h[s].pose, sizeof(float) * 3);
+        if (covs_out) memcpy(covs_out + 9 * s, h[s].cov, sizeof(float) * 9);
+        if (did_update_out) did_update_out[s] = h[s].do_update;
+        if (cells_out) cells_out[s] = (int64_t)(h[s].do_update ? h[s].step_cells : 0);
+    }
+    return HS_OK;
+}
+
+int hs_get_device_buffers(hs_ctx *c, void **cells, size_t *cells_bytes, size_t *stream_cells)
+{
+    if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    if (cells) *cells = c->d_cells;
+    if (cells_bytes) *cells_bytes = c->cells_bytes;
+    if (stream_cells) *stream_cells = c->geom.stream_cells;
+    return HS_OK;
+}
+
+void *hs_get_stream(hs_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int hs_set_timing(hs_ctx *c, int enable)
+{
+    if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    c->timing = enable != 0;
+    return HS_OK;
+}
+
+int hs_get_kernel_times(hs_ctx *c, double ms_out[4], int64_t launches_out[4], int reset)
+{
+    if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    for (auto &p : c->ev_used) {
+        HCHK(hipEventSynchronize(p.b));
+        float ms = 0.0f;
+        HCHK(hipEventElapsedTime(&ms, p.a, p.b));
+        c->acc_ms[p.kernel] += ms;
+        c->acc_n[p.kernel] += 1;
+        c->ev_free.push_back(p);
+    }
+    c->ev_used.clear();
+    for (int k = 0; k < NKERN; ++k) {
+        if (ms_out) ms_out[k] = c->acc_ms[k];
+        if (launches_out) launches_out[k] = c->acc_n[k];
+        if (reset) {
+            c->acc_ms[k] = 0.0;
+            c->acc_n[k] = 0;
+        }
+    }
+    return HS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,261 @@
+"""Host-side mirror of the reference's Hector interface over the MI355X C-ABI (include/slam2d/hector.h).
+
+Reference classes mirrored (lesson4/include/lesson4/hector_mapping/):
+  * DataContainer          scan/DataPointContainer.h:37-95   (points in map scale + origo)
+  * HectorSlamProcessor    slam_main/HectorSlamProcessor.h:54-149
+  * MapRepresentationInterface (slam_main/MapRepresentationInterface.h:44-69) is the seam the
+    device backend implements; `HectorFleet` exposes it for B independent streams at once.
+
+Method names follow the reference (camelCase) so parity tests read like the reference's API.
+Every compute call goes to the HIP library; there is no CPU path here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+_f = C.c_float
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class DataContainer:
+    """hectorslam::DataContainer (scan/DataPointContainer.h:37-95)."""
+
+    def __init__(self, size: int = 1000):
+        self._pts: list = []
+        self._arr = None
+        self.origo = np.zeros(2, np.float32)
+
+    def setFrom(self, other: "DataContainer", factor: float) -> None:  # :46-58
+        f = np.float32(factor)
+        self.origo = (other.getOrigo() * f).astype(np.float32)
+        self._arr = (other.points() * f).astype(np.float32)
+        self._pts = []
+
+    def add(self, p) -> None:  # :60-63
+        self._flush()
+        self._pts.append(np.asarray(p, np.float32))
+
+    def clear(self) -> None:
+        self._pts = []
+        self._arr = np.zeros((0, 2), np.float32)
+
+    def getSize(self) -> int:
+        return int(self.points().shape[0])
+
+    def getVecEntry(self, i: int) -> np.ndarray:
+        return self.points()[i]
+
+    def getOrigo(self) -> np.ndarray:
+        return self.origo.copy()
+
+    def setOrigo(self, o) -> None:
+        self.origo = np.asarray(o, np.float32).reshape(2)
+
+    # helpers
+    def _flush(self):
+        if self._arr is not None and len(self._arr):
+            self._pts = list(self._arr)
+        self._arr = None
+
+    def points(self) -> np.ndarray:
+        if self._arr is None:
+            self._arr = np.asarray(self._pts, np.float32).reshape(-1, 2) if self._pts else np.zeros((0, 2), np.float32)
+        return self._arr
+
+    @staticmethod
+    def from_points(pts, origo=(0.0, 0.0)) -> "DataContainer":
+        d = DataContainer()
+        d._arr = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+        d.setOrigo(origo)
+        return d
+
+
+class HectorFleet:
+    """B independent Hector SLAM streams resident in HBM (one MapRepMultiMap pyramid each)."""
+
+    def __init__(self, num_streams=1, map_resolution=0.05, map_size=2048, map_start=(0.5, 0.5), levels=3,
+                 max_points=1081, map_size_y=None):
+        self.L = _lib.lib()
+        self.B = int(num_streams)
+        self.levels = int(levels)
+        self.max_points = int(max_points)
+        h = C.c_void_p()
+        sy = map_size if map_size_y is None else map_size_y
+        check(self.L.hs_create(C.byref(h), self.B, _f(map_resolution), int(map_size), int(sy), _f(map_start[0]),
+                               _f(map_start[1]), self.levels, self.max_points), "hs_create")
+        self.h = h
+
+    # ---------------------------------------------------------------- lifecycle
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.hs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        check(self.L.hs_reset(self.h), "hs_reset")
+
+    def set_update_factors(self, free_factor: float, occupied_factor: float):
+        check(self.L.hs_set_update_factors(self.h, _f(free_factor), _f(occupied_factor)), "hs_set_update_factors")
+
+    def set_thresholds(self, min_dist: float, min_angle: float):
+        check(self.L.hs_set_map_update_thresholds(self.h, _f(min_dist), _f(min_angle)), "hs_set_map_update_thresholds")
+
+    # ---------------------------------------------------------------- single-stream (host buffers)
+    def update(self, stream: int, pts, origo=(0.0, 0.0), hint=None, map_without_matching=False):
+        pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+        pose = np.zeros(3, np.float32)
+        cov = np.zeros(9, np.float32)
+        did = C.c_int()
+        hp = None
+        if hint is not None:
+            hint = np.ascontiguousarray(hint, np.float32)
+            hp = _fp(hint)
+        check(self.L.hs_update(self.h, stream, _fp(pts), pts.shape[0], _f(origo[0]), _f(origo[1]), hp,
+                               1 if map_without_matching else 0, _fp(pose), _fp(cov), C.byref(did)), "hs_update")
+        return pose, cov.reshape(3, 3), bool(did.value)
+
+    def match(self, stream: int, pts, hint, origo=(0.0, 0.0)):
+        pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+        hint = np.ascontiguousarray(hint, np.float32)
+        pose = np.zeros(3, np.float32)
+        cov = np.zeros(9, np.float32)
+        check(self.L.hs_match(self.h, stream, _fp(pts), pts.shape[0], _f(origo[0]), _f(origo[1]), _fp(hint),
+                              _fp(pose), _fp(cov)), "hs_match")
+        return pose, cov.reshape(3, 3)
+
+    def update_by_scan(self, stream: int, pts, pose, origo=(0.0, 0.0)):
+        pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+        pose = np.ascontiguousarray(pose, np.float32)
+        check(self.L.hs_update_by_scan(self.h, stream, _fp(pts), pts.shape[0], _f(origo[0]), _f(origo[1]),
+                                       _fp(pose)), "hs_update_by_scan")
+
+    def last_pose(self, stream: int = 0):
+        pose = np.zeros(3, np.float32)
+        cov = np.zeros(9, np.float32)
+        check(self.L.hs_get_last_pose(self.h, stream, _fp(pose), _fp(cov)), "hs_get_last_pose")
+        return pose, cov.reshape(3, 3)
+
+    def map_info(self, level: int = 0):
+        sx, sy, cl = C.c_int(), C.c_int(), C.c_float()
+        org = np.zeros(2, np.float32)
+        check(self.L.hs_get_map_info(self.h, level, C.byref(sx), C.byref(sy), C.byref(cl), _fp(org)), "hs_get_map_info")
+        return sx.value, sy.value, cl.value, org
+
+    def scale_to_map(self) -> float:
+        s = C.c_float()
+        check(self.L.hs_get_scale_to_map(self.h, C.byref(s)), "hs_get_scale_to_map")
+        return s.value
+
+    def get_map(self, stream: int = 0, level: int = 0, want_occ=True, want_raw=True):
+        sx, sy, _, _ = self.map_info(level)
+        occ = np.empty(sx * sy, np.int8) if want_occ else None
+        l = np.empty(sx * sy, np.float32) if want_raw else None
+        u = np.empty(sx * sy, np.int32) if want_raw else None
+        ui = C.c_int()
+        check(self.L.hs_get_map(self.h, stream, level, _fp(occ) if want_occ else None, _fp(l) if want_raw else None,
+                                _fp(u) if want_raw else None, C.byref(ui)), "hs_get_map")
+        r = {"update_index": ui.value}
+        if want_occ:
+            r["occ"] = occ.reshape(sy, sx)
+        if want_raw:
+            r["logodds"] = l.reshape(sy, sx)
+            r["upd"] = u.reshape(sy, sx)
+        return r
+
+    def set_map(self, stream: int, level: int, logodds, upd):
+        l = np.ascontiguousarray(logodds, np.float32)
+        u = np.ascontiguousarray(upd, np.int32)
+        check(self.L.hs_set_map(self.h, stream, level, _fp(l), _fp(u)), "hs_set_map")
+
+    # ---------------------------------------------------------------- batched device path
+    def step_device(self, d_xy: int, xy_stride: int, d_n: int, d_origo: int = 0, d_hints: int = 0,
+                    stream_begin: int = 0, count: int | None = None, hip_stream: int = 0):
+        """One HectorSlamProcessor::update for every stream; pointers are device addresses (ints)."""
+        count = self.B - stream_begin if count is None else count
+        check(self.L.hs_step_batch_device(self.h, stream_begin, count, C.c_void_p(d_xy), int(xy_stride),
+                                          C.c_void_p(d_n), C.c_void_p(d_origo or None), C.c_void_p(d_hints or None),
+                                          C.c_void_p(hip_stream or None)), "hs_step_batch_device")
+
+    def poses(self):
+        p = np.zeros((self.B, 3), np.float32)
+        cv = np.zeros((self.B, 9), np.float32)
+        d = np.zeros(self.B, np.int32)
+        cells = np.zeros(self.B, np.int64)
+        check(self.L.hs_get_poses(self.h, _fp(p), _fp(cv), _fp(d), _fp(cells)), "hs_get_poses")
+        return p, cv.reshape(self.B, 3, 3), d.astype(bool), cells
+
+    def stream_handle(self) -> int:
+        return int(self.L.hs_get_stream(self.h) or 0)
+
+    def set_timing(self, enable: bool):
+        check(self.L.hs_set_timing(self.h, 1 if enable else 0), "hs_set_timing")
+
+    def kernel_times(self, reset=True):
+        ms = np.zeros(4, np.float64)
+        n = np.zeros(4, np.int64)
+        check(self.L.hs_get_kernel_times(self.h, _fp(ms), _fp(n), 1 if reset else 0), "hs_get_kernel_times")
+        names = ("match", "mark_hits", "free_cells", "resolve_hits")
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}
+
+
+class HectorSlamProcessor:
+    """hectorslam::HectorSlamProcessor (slam_main/HectorSlamProcessor.h:54-149), device-backed."""
+
+    def __init__(self, mapResolution=0.05, mapSizeX=2048, mapSizeY=2048, startCoords=(0.5, 0.5), multi_res_size=3,
+                 max_points=4096):
+        self.fleet = HectorFleet(1, mapResolution, mapSizeX, startCoords, multi_res_size, max_points,
+                                 map_size_y=mapSizeY)
+        self._cov = np.zeros((3, 3), np.float32)
+
+    def update(self, dataContainer: DataContainer, poseHintWorld, map_without_matching=False):  # :81-108
+        pose, cov, _ = self.fleet.update(0, dataContainer.points(), dataContainer.getOrigo(), poseHintWorld,
+                                         map_without_matching)
+        return pose
+
+    def reset(self):  # :111-117
+        self.fleet.reset()
+
+    def getLastScanMatchPose(self):
+        return self.fleet.last_pose(0)[0]
+
+    def getLastScanMatchCovariance(self):
+        return self.fleet.last_pose(0)[1]
+
+    def getScaleToMap(self) -> float:
+        return self.fleet.scale_to_map()
+
+    def getMapLevels(self) -> int:
+        return self.fleet.levels
+
+    def getGridMap(self, mapLevel=0):
+        return self.fleet.get_map(0, mapLevel)
+
+    def setUpdateFactorFree(self, free_factor):
+        self._free = free_factor
+        self.fleet.set_update_factors(free_factor, getattr(self, "_occ", 0.6))
+
+    def setUpdateFactorOccupied(self, occupied_factor):
+        self._occ = occupied_factor
+        self.fleet.set_update_factors(getattr(self, "_free", 0.4), occupied_factor)
+
+    def setMapUpdateMinDistDiff(self, minDist):
+        self._dist = minDist
+        self.fleet.set_thresholds(minDist, getattr(self, "_ang", 0.13))
+
+    def setMapUpdateMinAngleDiff(self, angleChange):
+        self._ang = angleChange
+        self.fleet.set_thresholds(getattr(self, "_dist", 0.4), angleChange)

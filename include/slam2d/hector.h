@@ -1,0 +1,118 @@
+/* include/slam2d/hector.h -- C-ABI of the MI355X Hector scan-matching + occupancy-grid path.
+ *
+ * Drop-in boundary: the reference's only polymorphic seam on this path is
+ * hectorslam::MapRepresentationInterface (lesson4/include/lesson4/hector_mapping/slam_main/
+ * MapRepresentationInterface.h:44-69), owned by HectorSlamProcessor (HectorSlamProcessor.h:61).
+ * Each entry point below names the reference member it replaces.  INTEGRATION.md shows the C++
+ * adapter `MapRepHip : MapRepresentationInterface` a maintainer would add on the ROS side.
+ *
+ * Conventions
+ *   - plain C types only; poses are float[3] (x, y, theta) in world metres/radians, covariance a
+ *     row-major float[9], scan points float[2*n] in map scale (DataContainer: point * scaleToMap,
+ *     hector_slam.cc:356) with origo (ox, oy) also in map scale (hector_slam.cc:329).
+ *   - every function returns HS_OK (0) or a negative HS_E* code; hs_last_error() describes it.
+ *     No exceptions cross the boundary.  The reference itself has no error reporting; its silent
+ *     semantics are kept (empty scan -> hint, out-of-map beam -> skipped, singular H -> no step).
+ *   - a context holds `num_streams` independent SLAM streams (one map pyramid each) resident in HBM.
+ *     num_streams = 1 is the ROS drop-in; > 1 is the batched throughput path.  A context is not
+ *     thread-safe: serialise calls (the reference serialises on the ROS spin thread).
+ *   - host-pointer entry points copy through pinned staging and synchronise; *_device entry points
+ *     take device pointers and a hipStream_t (as void*, NULL = the context's own stream) and do not
+ *     synchronise.
+ */
+#ifndef SLAM2D_HECTOR_H
+#define SLAM2D_HECTOR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HS_OK 0
+#define HS_EINVAL (-1)
+#define HS_EHIP (-2)
+#define HS_ENOMEM (-3)
+#define HS_ENODEV (-4)
+
+#define HS_MAX_LEVELS 8
+
+typedef struct hs_ctx hs_ctx;
+
+/* Version / self-description of the built library. */
+const char *hs_version(void);
+const char *hs_last_error(void);
+
+/* HectorSlamProcessor ctor + MapRepMultiMap ctor (HectorSlamProcessor.h:57-68, MapRepMultiMap.h:57-90).
+ * map_resolution/map_size/start/levels are the ROS params map_resolution, map_size, map_start_x/y,
+ * map_multi_res_levels (hector_slam.cc:138-142).  max_points bounds the scan size (>= 1). */
+int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_x, int map_size_y,
+              float map_start_x, float map_start_y, int levels, int max_points);
+/* ~HectorSlamProcessor (HectorSlamProcessor.h:70-73) */
+int hs_destroy(hs_ctx *ctx);
+/* HectorSlamProcessor::reset (HectorSlamProcessor.h:111-117) for every stream */
+int hs_reset(hs_ctx *ctx);
+/* MapRepresentationInterface::setUpdateFactorFree / setUpdateFactorOccupied (:67-68) */
+int hs_set_update_factors(hs_ctx *ctx, float free_factor, float occupied_factor);
+/* HectorSlamProcessor::setMapUpdateMinDistDiff / setMapUpdateMinAngleDiff (HectorSlamProcessor.h:137-138) */
+int hs_set_map_update_thresholds(hs_ctx *ctx, float min_dist, float min_angle);
+
+/* MapRepresentationInterface::getScaleToMap / getMapLevels (:50-52) */
+int hs_get_scale_to_map(hs_ctx *ctx, float *scale_out);
+int hs_get_map_levels(hs_ctx *ctx, int *levels_out);
+/* GridMap dimensions / cell length / world origin of cell (0,0) for level (GridMapBase.h:85-87,301-304) */
+int hs_get_map_info(hs_ctx *ctx, int level, int *size_x, int *size_y, float *cell_length, float *origin_xy);
+
+/* HectorSlamProcessor::update (HectorSlamProcessor.h:81-108) on one stream: match coarse->fine,
+ * store the pose, update every level if the pose moved more than the thresholds (or
+ * map_without_matching).  hint NULL = the stream's last scan-match pose (hector_slam.cc:201).
+ * did_update_out may be NULL. */
+int hs_update(hs_ctx *ctx, int stream, const float *xy, int n, float ox, float oy, const float *hint,
+              int map_without_matching, float pose_out[3], float cov_out[9], int *did_update_out);
+/* MapRepresentationInterface::matchData (MapRepMultiMap.h:144-167): no state change */
+int hs_match(hs_ctx *ctx, int stream, const float *xy, int n, float ox, float oy, const float hint[3],
+             float pose_out[3], float cov_out[9]);
+/* MapRepresentationInterface::updateByScan + onMapUpdated (MapRepMultiMap.h:174-191, :127-135) */
+int hs_update_by_scan(hs_ctx *ctx, int stream, const float *xy, int n, float ox, float oy, const float pose[3]);
+
+/* HectorSlamProcessor::getLastScanMatchPose / getLastScanMatchCovariance (HectorSlamProcessor.h:120-122) */
+int hs_get_last_pose(hs_ctx *ctx, int stream, float pose_out[3], float cov_out[9]);
+
+/* getGridMap(level) read-out (MapRepresentationInterface.h:54) in the publishMap format
+ * (hector_slam.cc:287-304): occ_out int8 row-major (-1 unknown, 0 free, 100 occupied); optional raw
+ * log-odds and per-cell updateIndex; update_index_out = GridMapBase::getUpdateIndex (GridMapBase.h:334).
+ * Any output pointer may be NULL. */
+int hs_get_map(hs_ctx *ctx, int stream, int level, int8_t *occ_out, float *logodds_out, int32_t *cell_update_index_out,
+               int *update_index_out);
+/* Overwrite one level's cells (log-odds + updateIndex); for tests and map reload. */
+int hs_set_map(hs_ctx *ctx, int stream, int level, const float *logodds, const int32_t *cell_update_index);
+
+/* ---- batched, device-resident throughput path ------------------------------------------------ */
+/* One HectorSlamProcessor::update for every stream in [stream_begin, stream_begin+count):
+ *   d_xy     : device float2 points, stream s at d_xy + 2*xy_stride*(s - stream_begin)
+ *   d_n      : device int per stream (0 <= n <= max_points)
+ *   d_origo  : device float2 per stream, or NULL for (0,0)
+ *   d_hints  : device float3 per stream, or NULL = each stream's last pose
+ * Results stay on device; read them with hs_get_poses (synchronising) when needed. */
+int hs_step_batch_device(hs_ctx *ctx, int stream_begin, int count, const float *d_xy, int xy_stride, const int *d_n,
+                         const float *d_origo, const float *d_hints, void *hip_stream);
+/* Copy poses (float3), covariances (float9), did-update flags and Σ cells traversed of the last
+ * step (int64, Σ_levels Σ_valid rays (abs_da + 1)) for every stream.  Any pointer may be NULL. */
+int hs_get_poses(hs_ctx *ctx, float *poses_out, float *covs_out, int *did_update_out, int64_t *cells_traversed_out);
+/* Device pointer of the per-stream state array and of the cell storage (for zero-copy consumers). */
+int hs_get_device_buffers(hs_ctx *ctx, void **cells, size_t *cells_bytes, size_t *stream_cells);
+/* The context's own HIP stream (hipStream_t as void*). */
+void *hs_get_stream(hs_ctx *ctx);
+
+/* ---- measurement ----------------------------------------------------------------------------- */
+/* Kernel timing with HIP events recorded on the launch stream around every kernel of every step
+ * (enable = 1).  hs_get_kernel_times fills, for the 4 kernels {match, mark_hits, free_cells,
+ * resolve_hits}, the accumulated milliseconds and launch counts since the last reset (synchronises). */
+int hs_set_timing(hs_ctx *ctx, int enable);
+int hs_get_kernel_times(hs_ctx *ctx, double ms_out[4], int64_t launches_out[4], int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

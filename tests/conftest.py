@@ -1,0 +1,44 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "creating-2d-laser-slam-from-scratch_amd")
+for p in (os.path.join(PKG, "python"), os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
+    config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _built_oracle():
+    """Build the CPU checkers if they are missing (gcc is available on both machines)."""
+    need = [os.path.join(REPO, "oracle", "build", n) for n in ("libhector_oracle.so", "libgmapping_oracle.so")]
+    if not all(os.path.exists(p) for p in need):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "oracle"])
+    yield
+
+
+def gpu_available() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    if not gpu_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    import slam2d
+
+    slam2d.lib()
+    return True

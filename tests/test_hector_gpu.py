@@ -1,0 +1,243 @@
+"""GPU parity of the Hector path: HIP kernels (through the C-ABI) vs the CPU oracle.
+
+Bar (BASELINE.json north_star):
+  * integer / byte work bit-exact: every cell's updateIndex, the Bresenham cell count ΣL, the
+    did-update gate, the map update index;
+  * log-odds floats bit-exact against the oracle run in the kernel's reduction order
+    (reduce_threads=256), because the update replays the reference's per-cell float sequence;
+  * pose within POSE_TOL_M / POSE_TOL_RAD of the oracle in the reference's sequential order
+    (the Hessian sums are reassociated by the parallel reduction).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from slam2d import synth
+from slam2d.hector import DataContainer, HectorFleet, HectorSlamProcessor
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL_M = 1e-4    # north_star: pose error <= 1e-4 m
+POSE_TOL_RAD = 1e-4  # north_star: pose error <= 1e-4 rad
+T_RED = 256          # hs_match_kernel workgroup size (reduction order)
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.int32)
+
+
+def _run_pair(levels, size, scans, n_scans=25, thresholds=(0.4, 0.9), stream=0, origo=(0.0, 0.0)):
+    fleet = HectorFleet(1, 0.05, size, (0.5, 0.5), levels, max_points=1081)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(*thresholds)
+    ora = O.HectorOracle(0.05, size, (0.5, 0.5), levels, reduce_threads=T_RED)
+    ora.set_update_factors(0.4, 0.9)
+    ora.set_thresholds(*thresholds)
+    for k in range(n_scans):
+        pts = scans.points[stream, k, : scans.counts[stream, k]]
+        gp, gc, gd = fleet.update(0, pts, origo)
+        op, oc, od = ora.process(pts, origo)
+        assert gd == od, f"scan {k}: did_update {gd} vs {od}"
+        np.testing.assert_array_equal(_bits(gp), _bits(op), err_msg=f"scan {k} pose")
+        np.testing.assert_array_equal(_bits(gc), _bits(oc), err_msg=f"scan {k} cov")
+    for lvl in range(levels):
+        m = fleet.get_map(0, lvl)
+        ol, ou = ora.level(lvl)
+        np.testing.assert_array_equal(m["upd"], ou, err_msg=f"level {lvl} updateIndex")
+        np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol), err_msg=f"level {lvl} log-odds bits")
+        np.testing.assert_array_equal(m["occ"], ora.publish(lvl), err_msg=f"level {lvl} publish")
+        assert m["update_index"] == ora.update_index(lvl)
+    return fleet, ora
+
+
+@pytest.fixture(scope="module")
+def scans():
+    return synth.make_streams(4, 40)
+
+
+def test_single_level_1024_bitexact(gpu, scans):
+    _run_pair(1, 1024, scans, n_scans=30)
+
+
+def test_three_level_2048_bitexact(gpu, scans):
+    _run_pair(3, 2048, scans, n_scans=20, stream=1)
+
+
+def test_force_update_every_scan(gpu, scans):
+    # benchmark mode: thresholds < 0 force a map update on every scan
+    _run_pair(2, 512, scans, n_scans=20, thresholds=(-1.0, -1.0), stream=2)
+
+
+def test_origo_offset(gpu, scans):
+    _run_pair(2, 1024, scans, n_scans=12, origo=(3.25, -1.5), stream=3)
+
+
+def test_out_of_map_beams_small_map(gpu, scans):
+    # 256^2 at 5 cm = 12.8 m: many beams end outside and are cancelled (OccGridMapBase.h:226-238)
+    _run_pair(1, 256, scans, n_scans=15, thresholds=(-1.0, -1.0))
+
+
+def test_pose_tolerance_vs_reference_order(gpu, scans):
+    """GPU trajectory vs the oracle in the reference's sequential summation order."""
+    n = 30
+    fleet = HectorFleet(1, 0.05, 2048, (0.5, 0.5), 3, max_points=1081)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(0.4, 0.9)
+    ref = O.HectorOracle(0.05, 2048, (0.5, 0.5), 3, reduce_threads=0)
+    ref.set_update_factors(0.4, 0.9)
+    ref.set_thresholds(0.4, 0.9)
+    errs = []
+    for k in range(n):
+        pts = scans.points[0, k, : scans.counts[0, k]]
+        gp, _, _ = fleet.update(0, pts)
+        rp, _, _ = ref.process(pts)
+        errs.append(np.abs(gp.astype(np.float64) - rp.astype(np.float64)))
+    e = np.max(errs, axis=0)
+    assert e[0] <= POSE_TOL_M and e[1] <= POSE_TOL_M and e[2] <= POSE_TOL_RAD, e
+
+
+def test_match_only_and_update_by_scan(gpu, scans):
+    """MapRepresentationInterface::matchData / updateByScan entry points."""
+    fleet = HectorFleet(1, 0.05, 1024, (0.5, 0.5), 2, max_points=1081)
+    ora = O.HectorOracle(0.05, 1024, (0.5, 0.5), 2, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+    pose = np.zeros(3, np.float32)
+    for k in range(8):
+        pts = scans.points[0, k, : scans.counts[0, k]]
+        gp, gc = fleet.match(0, pts, pose)
+        op, oc = ora.match(pts, pose)
+        np.testing.assert_array_equal(_bits(gp), _bits(op))
+        np.testing.assert_array_equal(_bits(gc), _bits(oc))
+        fleet.update_by_scan(0, pts, gp)
+        ora.update_by_scan(pts, op)
+        pose = op
+    for lvl in range(2):
+        m = fleet.get_map(0, lvl)
+        ol, ou = ora.level(lvl)
+        np.testing.assert_array_equal(m["upd"], ou)
+        np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))
+
+
+def test_map_without_matching_and_empty_scan(gpu, scans):
+    fleet = HectorFleet(1, 0.05, 512, (0.5, 0.5), 1, max_points=1081)
+    ora = O.HectorOracle(0.05, 512, (0.5, 0.5), 1, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(0.4, 0.9)
+    hint = np.array([0.1, -0.05, 0.02], np.float32)
+    pts = scans.points[0, 0, : scans.counts[0, 0]]
+    gp, _, gd = fleet.update(0, pts, hint=hint, map_without_matching=True)
+    op, _, od = ora.process(pts, hint=hint, map_without_matching=True)
+    assert gd and od
+    np.testing.assert_array_equal(_bits(gp), _bits(op))
+    # empty scan: pose = hint, no GN step (ScanMatcher.h:65, :96)
+    e = np.zeros((0, 2), np.float32)
+    gp, _, gd = fleet.update(0, e, hint=hint)
+    op, _, od = ora.process(e, hint=hint)
+    np.testing.assert_array_equal(_bits(gp), _bits(op))
+    assert gd == od
+    m = fleet.get_map(0, 0)
+    ol, ou = ora.level(0)
+    np.testing.assert_array_equal(m["upd"], ou)
+    np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))
+
+
+def test_degenerate_rays(gpu):
+    """Zero-length beams (begin == end, skipped), 1-cell rays, rays along axes and diagonals."""
+    pts = []
+    for r in (0.0, 0.3, 0.6, 1.0, 1.5, 7.0, 40.0):
+        for a in np.linspace(-np.pi, np.pi, 37):
+            pts.append((r * np.cos(a), r * np.sin(a)))
+    pts += [(5.0, 0.0), (0.0, 5.0), (-5.0, 0.0), (0.0, -5.0), (5.0, 5.0), (-5.0, 5.0), (5.0, -5.0), (-5.0, -5.0)]
+    pts = np.asarray(pts, np.float32)
+    fleet = HectorFleet(1, 0.05, 128, (0.5, 0.5), 2, max_points=len(pts))
+    ora = O.HectorOracle(0.05, 128, (0.5, 0.5), 2, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(-1.0, -1.0)
+    for k, pose in enumerate([(0.0, 0.0, 0.0), (0.013, -0.021, 0.3), (0.4, 0.2, -1.2), (-1.0, 1.0, 2.9)]):
+        pose = np.asarray(pose, np.float32)
+        fleet.update_by_scan(0, pts, pose, origo=(0.2 * k, -0.1 * k))
+        ora.update_by_scan(pts, pose, origo=(0.2 * k, -0.1 * k))
+    for lvl in range(2):
+        m = fleet.get_map(0, lvl)
+        ol, ou = ora.level(lvl)
+        np.testing.assert_array_equal(m["upd"], ou)
+        np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))
+
+
+def test_reset(gpu, scans):
+    fleet = HectorFleet(1, 0.05, 256, (0.5, 0.5), 1, max_points=1081)
+    pts = scans.points[0, 0, : scans.counts[0, 0]]
+    fleet.update(0, pts)
+    fleet.reset()
+    m = fleet.get_map(0, 0)
+    assert np.all(m["logodds"] == 0.0) and np.all(m["upd"] == -1) and m["update_index"] == -1
+    assert np.all(fleet.last_pose(0)[0] == 0.0)
+
+
+def test_processor_mirror(gpu, scans):
+    """HectorSlamProcessor mirror (reference API names) over DataContainer."""
+    proc = HectorSlamProcessor(0.05, 1024, 1024, (0.5, 0.5), 2, max_points=1081)
+    proc.setUpdateFactorFree(0.4)
+    proc.setUpdateFactorOccupied(0.9)
+    proc.setMapUpdateMinDistDiff(0.4)
+    proc.setMapUpdateMinAngleDiff(0.9)
+    ora = O.HectorOracle(0.05, 1024, (0.5, 0.5), 2, reduce_threads=T_RED)
+    ora.set_update_factors(0.4, 0.9)
+    ora.set_thresholds(0.4, 0.9)
+    for k in range(10):
+        dc = DataContainer.from_points(scans.points[1, k, : scans.counts[1, k]])
+        p = proc.update(dc, proc.getLastScanMatchPose())
+        op, _, _ = ora.process(dc.points())
+        np.testing.assert_array_equal(_bits(p), _bits(op))
+    assert proc.getMapLevels() == 2 and proc.getScaleToMap() == 20.0
+    g = proc.getGridMap(0)
+    np.testing.assert_array_equal(g["occ"], ora.publish(0))
+
+
+def _torch_dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def test_batched_device_ragged(gpu):
+    """hs_step_batch_device over B streams with ragged scan sizes (incl. an empty scan) == per-stream oracle."""
+    import torch
+
+    B, T = 6, 12
+    S = synth.make_streams(B, T, seed=777)
+    counts = S.counts.copy()
+    counts[2, 5] = 0             # empty scan
+    counts[4, :] = np.minimum(counts[4, :], 300)  # truncated scans
+    fleet = HectorFleet(B, 0.05, 1024, (0.5, 0.5), 2, max_points=1081)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(0.4, 0.9)
+    oras = []
+    for s in range(B):
+        o = O.HectorOracle(0.05, 1024, (0.5, 0.5), 2, reduce_threads=T_RED)
+        o.set_update_factors(0.4, 0.9)
+        o.set_thresholds(0.4, 0.9)
+        oras.append(o)
+    stride = 1081
+    for t in range(T):
+        d_xy = _torch_dev(S.points[:, t])
+        d_n = _torch_dev(counts[:, t].astype(np.int32))
+        fleet.step_device(d_xy.data_ptr(), stride, d_n.data_ptr())
+        torch.cuda.synchronize()
+        gp, gc, gd, cells = fleet.poses()
+        for s in range(B):
+            pts = S.points[s, t, : counts[s, t]]
+            op, oc, od = oras[s].process(pts)
+            assert gd[s] == od, (t, s)
+            np.testing.assert_array_equal(_bits(gp[s]), _bits(op), err_msg=f"t={t} s={s}")
+            if od:
+                assert cells[s] == oras[s].sum_L(), (t, s, cells[s], oras[s].sum_L())
+    for s in range(B):
+        for lvl in range(2):
+            m = fleet.get_map(s, lvl)
+            ol, ou = oras[s].level(lvl)
+            np.testing.assert_array_equal(m["upd"], ou, err_msg=f"s={s} lvl={lvl}")
+            np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol), err_msg=f"s={s} lvl={lvl}")

@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py -- Hector scan-match + grid-update throughput on MI355X (BASELINE.json metric).
+
+One step = one HectorSlamProcessor::update (match coarse->fine + log-odds raycast update of every
+pyramid level) for each of B independent scan streams resident in HBM (inputs uploaded before the
+timed region).  Benchmark mode forces a map update on every scan (thresholds < 0).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--streams B] [--config northstar|c2|c3]
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU; each rank runs its own B streams
+(replicas only -- the Hector path has no cross-stream exchange), barrier + synchronize around the
+timed region, max time over ranks, value = total scans of all ranks / that time.
+
+Rank 0 prints ONE JSON line with value, roofline (dominant kernel, HIP-event timed inside the timed
+region) and cpu_baseline (the CPU oracle, single core, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "creating-2d-laser-slam-from-scratch_amd")
+sys.path.insert(0, os.path.join(PKG, "python"))
+
+METRIC = "scans/sec (1081-beam) Hector match+grid-update @1 GPU; pose RMSE vs ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+
+CONFIGS = {
+    # hector_slam.launch defaults (hector_slam.cc:138-142): 2048^2, 3 levels -- the north-star grid
+    "northstar": dict(map_size=2048, levels=3, streams=1024),
+    # BASELINE configs[1]: single-res 1024^2
+    "c2": dict(map_size=1024, levels=1, streams=1024),
+    # BASELINE configs[2]: 3-level 4096^2
+    "c3": dict(map_size=4096, levels=3, streams=256),
+}
+KERNELS = ("match", "update")
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(ctr: dict, levels: int) -> dict:
+    """B_match = Σ_l (1+maxIter_l) N_l 24 B (8 B point + 4 corners x 4 B);
+    B_update = ΣL 16 B (8 B LogOddsCell read + 8 B write per traversed cell, ΣL = Σ (abs_da+1))."""
+    b_match = ctr["gn_points"] * 24
+    b_update = ctr["cells"] * 16
+    return {"match": b_match, "update": b_update, "total": b_match + b_update,
+            "read_only": b_match + ctr["cells"] * 8}
+
+
+def cpu_baseline(cfg, seconds=10.0, max_scans=4000):
+    """Time the CPU oracle (C restatement at -O2, reference sequential order, 1 core) on a bounded
+    sample of the same workload: one stream, consecutive scans, forced map update each scan."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    from slam2d import synth
+
+    n_scans = 600
+    S = synth.make_streams(1, n_scans, seed=999)
+    h = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0)
+    h.set_update_factors(0.4, 0.9)
+    h.set_thresholds(-1.0, -1.0)
+    done = 0
+    t0 = time.perf_counter()
+    while done < n_scans and time.perf_counter() - t0 < seconds:
+        h.process(S.points[0, done, : S.counts[0, done]])
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "scans/s", "cores": 1, "kind": "port",
+            "sample": f"1 stream x {done} consecutive synthetic 1081-beam scans, {cfg['map_size']}^2 x "
+                      f"{cfg['levels']} levels, forced map update, oracle/hector_oracle.c -O2 single thread"}
+
+
+def pose_check(cfg, n_scans=40):
+    """Pose error of the GPU path vs the oracle in the reference's sequential summation order
+    (the metric's 'pose RMSE vs ref'), one stream, forced updates."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    from slam2d import synth
+    from slam2d.hector import HectorFleet
+
+    S = synth.make_streams(1, n_scans, seed=4242)
+    f = HectorFleet(1, 0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], max_points=1081)
+    r = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0)
+    for x in (f, r):
+        x.set_update_factors(0.4, 0.9)
+        x.set_thresholds(-1.0, -1.0)
+    e = []
+    for k in range(n_scans):
+        pts = S.points[0, k, : S.counts[0, k]]
+        gp, _, _ = f.update(0, pts)
+        rp, _, _ = r.process(pts)
+        e.append(gp.astype(np.float64) - rp.astype(np.float64))
+    f.close()
+    e = np.asarray(e)
+    return {"scans": n_scans, "rmse_xy_m": float(np.sqrt(np.mean(e[:, 0] ** 2 + e[:, 1] ** 2))),
+            "rmse_theta_rad": float(np.sqrt(np.mean(e[:, 2] ** 2))),
+            "max_abs_xy_m": float(np.abs(e[:, :2]).max()), "max_abs_theta_rad": float(np.abs(e[:, 2]).max()),
+            "tolerance": "1e-4 m / 1e-4 rad (north_star)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--streams", type=int, default=0, help="streams per GPU (0 = config default)")
+    ap.add_argument("--config", default="northstar", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from slam2d import synth
+    from slam2d.hector import HectorFleet
+
+    cfg = dict(CONFIGS[args.config])
+    B = args.streams or cfg["streams"]
+    K, W = args.steps, args.warmup
+    T = K + W
+
+    # ---- synthetic input, resident in HBM before timing: [step][stream][1081][2] ----
+    t0 = time.perf_counter()
+    S = synth.make_streams(B, T, seed=12345 + rank * B)
+    pts = np.ascontiguousarray(S.points.transpose(1, 0, 2, 3))
+    cnt = np.ascontiguousarray(S.counts.T.astype(np.int32))
+    d_pts = torch.from_numpy(pts).to(dev)
+    d_cnt = torch.from_numpy(cnt).to(dev)
+    log(f"[bench] rank {rank}: generated {B} streams x {T} scans in {time.perf_counter() - t0:.1f}s")
+
+    fleet = HectorFleet(B, 0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], max_points=1081)
+    fleet.set_update_factors(0.4, 0.9)   # hector_slam.cc:144-145
+    fleet.set_thresholds(-1.0, -1.0)     # benchmark mode: update every scan
+    hs = torch.cuda.current_stream(dev).cuda_stream
+    stride = pts.shape[2]
+    step_bytes = pts.shape[1] * pts.shape[2] * 8
+
+    def step(t):
+        fleet.step_device(d_pts.data_ptr() + t * step_bytes, stride, d_cnt[t].data_ptr(), hip_stream=hs)
+
+    for t in range(W):
+        step(t)
+    torch.cuda.synchronize()
+    fleet.counters(reset=True)
+    fleet.kernel_times(reset=True)
+    fleet.set_timing(not args.no_timing)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(W, T):
+        step(t)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    fleet.set_timing(False)
+    ktimes = fleet.kernel_times(reset=True)
+    ctr = fleet.counters(reset=True)
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    scans = torch.tensor([float(B * K)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(scans, op=dist.ReduceOp.SUM)
+    t_max = float(el.item())
+    total_scans = float(scans.item())
+    value = total_scans / t_max
+
+    if rank == 0:
+        ab = algorithmic_bytes(ctr, cfg["levels"])
+        roof = None
+        if not args.no_timing and ktimes["update"][1] > 0:
+            dom = max(KERNELS, key=lambda k: ktimes[k][0])
+            ms, nlaunch = ktimes[dom]
+            per_launch_bytes = ab[dom] / nlaunch
+            avg_s = ms / 1e3 / nlaunch
+            achieved = per_launch_bytes / avg_s / 1e9
+            roof = {"bound": "hbm", "kernel": f"hs_{dom}_kernel", "achieved": round(achieved, 2),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                    "traffic": None, "avg_launch_ms": round(ms / nlaunch, 5),
+                    "alg_bytes_per_launch": int(per_launch_bytes),
+                    "kernel_ms_per_step": {k: round(ktimes[k][0] / max(ktimes[k][1], 1), 5) for k in KERNELS},
+                    "whole_step_GBps": round(ab["total"] / K / (t_max / K) / 1e9, 2),
+                    "whole_step_frac": round(ab["total"] / t_max / 1e9 / HBM_PEAK_GBS, 5),
+                    "read_only_frac": round(ab["read_only"] / t_max / 1e9 / HBM_PEAK_GBS, 5),
+                    "alg_bytes_per_scan": int(ab["total"] / max(B * K, 1)),
+                    "cells_per_scan": round(ctr["cells"] / max(B * K, 1), 1)}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(cfg)
+        pose = pose_check(cfg) if world == 1 else None
+        out = {"metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K,
+               "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+               "config": {"workload": f"hector_slam match+update, {cfg['map_size']}x{cfg['map_size']} @0.05 m x "
+                                      f"{cfg['levels']} levels, 1081-beam scans, map update every scan",
+                          "config": args.config, "streams_per_gpu": B, "global_batch": B * world,
+                          "map_size": cfg["map_size"], "levels": cfg["levels"], "beams": 1081,
+                          "parallelism": f"replicas x{world}"},
+               "roofline": roof, "cpu_baseline": cpu, "pose_vs_ref": pose}
+        if cpu:
+            out["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    fleet.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

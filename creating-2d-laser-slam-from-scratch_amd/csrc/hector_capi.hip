@@ -36,7 +36,7 @@ int fail(int code, const char *what, hipError_t e = hipSuccess)
         if (_e != hipSuccess) return fail(HS_EHIP, #expr, _e); \
     } while (0)
 
-constexpr int NKERN = 4;
+constexpr int NKERN = 2;
 
 struct EventPair {
     hipEvent_t a, b;
@@ -63,8 +63,8 @@ struct hs_ctx {
     // timing
     bool timing = false;
     std::vector<EventPair> ev_used, ev_free;
-    double acc_ms[NKERN] = {0, 0, 0, 0};
-    int64_t acc_n[NKERN] = {0, 0, 0, 0};
+    double acc_ms[NKERN] = {0, 0};
+    int64_t acc_n[NKERN] = {0, 0};
 };
 
 namespace {
@@ -171,21 +171,10 @@ int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride
     end_timed(c, s);
     HCHK(hipGetLastError());
     if (mode == MODE_MATCH_ONLY) return HS_OK;
-    const int nb256 = (c->max_points + 255) / 256;
-    const int nb64 = (c->max_points + FREE_BEAMS - 1) / FREE_BEAMS;
+    const size_t shmem = sizeof(unsigned) * ((size_t)TILE_CELLS + (size_t)c->max_points);
     begin_timed(c, 1, s);
-    hipLaunchKernelGGL(hs_mark_hits_kernel, dim3(nb256, c->levels, count), dim3(256), 0, s, c->geom, c->d_cells,
-                       c->d_state, xy, xy_stride, begin);
-    end_timed(c, s);
-    HCHK(hipGetLastError());
-    begin_timed(c, 2, s);
-    hipLaunchKernelGGL(hs_free_cells_kernel, dim3(nb64, c->levels, count), dim3(256), 0, s, c->geom, c->d_cells,
-                       c->d_state, xy, xy_stride, begin);
-    end_timed(c, s);
-    HCHK(hipGetLastError());
-    begin_timed(c, 3, s);
-    hipLaunchKernelGGL(hs_resolve_hits_kernel, dim3(nb256, c->levels, count), dim3(256), 0, s, c->geom, c->d_cells,
-                       c->d_state, xy, xy_stride, begin);
+    hipLaunchKernelGGL(hs_update_kernel, dim3(count * c->levels), dim3(UPD_THREADS), shmem, s, c->geom, c->d_cells,
+                       c->d_state, xy, xy_stride, begin, count, c->max_points);
     end_timed(c, s);
     HCHK(hipGetLastError());
     return HS_OK;
@@ -218,7 +207,7 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
     if (!out) return fail(HS_EINVAL, "out is NULL");
     *out = nullptr;
     if (num_streams < 1 || levels < 1 || levels > HS_MAX_LEVELS || map_size_x < 2 || map_size_y < 2 ||
-        max_points < 1 || !(map_resolution > 0.0f))
+        map_size_x > 32768 || map_size_y > 32768 || max_points < 1 || max_points > 65535 || !(map_resolution > 0.0f))
         return fail(HS_EINVAL, "invalid hs_create arguments");
     if ((map_size_x >> (levels - 1)) < 2 || (map_size_y >> (levels - 1)) < 2)
         return fail(HS_EINVAL, "map too small for the requested number of levels");
@@ -472,6 +461,28 @@ int hs_get_poses(hs_ctx *c, float *poses_out, float *covs_out, int *did_update_o
     return HS_OK;
 }
 
+int hs_get_counters(hs_ctx *c, int64_t out[5], int reset)
+{
+    if (!c || !out) return fail(HS_EINVAL, "NULL argument");
+    std::vector<StreamState> h(c->B);
+    HCHK(hipStreamSynchronize(c->stream));
+    HCHK(hipDeviceSynchronize());
+    HCHK(hipMemcpy(h.data(), c->d_state, sizeof(StreamState) * c->B, hipMemcpyDeviceToHost));
+    for (int k = 0; k < 5; ++k) out[k] = 0;
+    for (int s = 0; s < c->B; ++s) {
+        out[0] += (int64_t)h[s].tot_cells;
+        out[1] += (int64_t)h[s].tot_rays;
+        out[2] += (int64_t)h[s].tot_gn_points;
+        out[3] += (int64_t)h[s].tot_updates;
+        out[4] += (int64_t)h[s].tot_steps;
+        if (reset) {
+            h[s].tot_cells = h[s].tot_rays = h[s].tot_gn_points = h[s].tot_updates = h[s].tot_steps = 0;
+        }
+    }
+    if (reset) HCHK(hipMemcpy(c->d_state, h.data(), sizeof(StreamState) * c->B, hipMemcpyHostToDevice));
+    return HS_OK;
+}
+
 int hs_get_device_buffers(hs_ctx *c, void **cells, size_t *cells_bytes, size_t *stream_cells)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
@@ -490,7 +501,7 @@ int hs_set_timing(hs_ctx *c, int enable)
     return HS_OK;
 }
 
-int hs_get_kernel_times(hs_ctx *c, double ms_out[4], int64_t launches_out[4], int reset)
+int hs_get_kernel_times(hs_ctx *c, double ms_out[2], int64_t launches_out[2], int reset)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
     for (auto &p : c->ev_used) {

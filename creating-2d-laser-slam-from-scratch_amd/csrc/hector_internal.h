@@ -60,6 +60,12 @@ struct alignas(16) StreamState {
     int n;                   // this step's point count
     int clamp_count;         // "SearchDir angle change too large" events (ScanMatcher.h:123-132)
     unsigned long long step_cells;  // Σ (abs_da + 1) of this step's valid rays, all levels
+    // cumulative counters since the last hs_reset_counters (algorithmic-byte accounting)
+    unsigned long long tot_cells;     // Σ (abs_da + 1)  (cells visited by the raycast)
+    unsigned long long tot_rays;      // valid rays drawn
+    unsigned long long tot_gn_points; // Σ over GN iterations of the points evaluated
+    unsigned long long tot_updates;   // map updates (steps with do_update)
+    unsigned long long tot_steps;     // steps
 };
 
 }  // namespace s2d

@@ -11,12 +11,12 @@
 // One step = one HectorSlamProcessor::update per stream (H/slam_main/HectorSlamProcessor.h:81-108):
 //   k1 hs_match_kernel      one 256-thread workgroup per stream: all levels coarse->fine, all
 //                           Gauss-Newton iterations, block reduction of H/b, 3x3 solve, gating.
-//   k2 hs_mark_hits_kernel  one thread per beam: end cell gets the "first hitting beam" marker.
-//   k3 hs_free_cells_kernel 64 beams per workgroup, the workgroup's free cells flattened over 256
-//                           threads (load balance); first touch applies l += lf exactly once.
-//   k4 hs_resolve_hits_kernel the first hitting beam finalises each hit cell.
-// k2..k4 reproduce the sequential per-cell float sequence of bresenhamCellFree/Occ
-// (H/map/OccGridMapBase.h:302-330) exactly; see DESIGN.md "once-per-scan semantics".
+//   k2 hs_update_kernel     one 256-thread workgroup per (stream, level): the scan's bounding box is
+//                           walked in 64x64-cell tiles; each ray's cells inside a tile come from the
+//                           closed-form Bresenham step range, the once-per-scan semantics of
+//                           bresenhamCellFree/Occ (H/map/OccGridMapBase.h:302-330) are resolved in
+//                           LDS, then touched cells get ONE coalesced 8-byte read-modify-write.
+//                           No global atomics; see DESIGN.md "once-per-scan semantics".
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -267,6 +267,12 @@ hs_match_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__
         for (int k = 0; k < 9; ++k) out_cov[9 * local + k] = cov[k];
     }
     st.clamp_count += clamps;
+    st.tot_steps += 1;
+    if (mode == MODE_PROCESS || mode == MODE_MATCH_ONLY) {
+        unsigned long long it = 0;
+        for (int lvl = 0; lvl < geom.levels; ++lvl) it += (lvl == 0 ? 6 : 4);
+        st.tot_gn_points += it * (unsigned long long)n;
+    }
     st.n = n;
     st.origo[0] = origo ? origo[local].x : 0.0f;
     st.origo[1] = origo ? origo[local].y : 0.0f;
@@ -295,20 +301,25 @@ hs_match_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__
         st.cur_update_index += 3;            // OccGridMapBase.h:167
         st.map_updates += 1;                 // GridMapBase::setUpdated (GridMapBase.h:333)
         st.step_cells = 0;
+        st.tot_updates += 1;
     }
 }
 
 // ------------------------------------------------------------------------------- ray geometry
 // OccGridMapBase::updateByScan (H/map/OccGridMapBase.h:118-161) + updateLineBresenhami (:220-267).
-// Bresenham step i (0..abs_da-1 free, abs_da = end) in closed form:
-//   cell_i = start + i*off_a + floor((e0 + i*abs_db) / abs_da) * off_b,  e0 = abs_da/2,
-// which equals bresenham2D's incremental error walk (:281-298): error stays in [0, abs_da).
-struct Ray {
-    int valid;
-    int start;
-    int end;
-    int abs_da, abs_db, e0, off_a, off_b;
-};
+// Every ray starts at the common begin cell; a ray is stored as its end cell (packed y<<16 | x) or
+// RAY_INVALID when updateByScan would skip it (begin == end :157, or begin/end outside :226-238).
+constexpr unsigned RAY_INVALID = 0xFFFFFFFFu;
+constexpr int TILE = 64;                 // tile edge (cells); a tile row = 64 x 8 B = 512 B
+constexpr int TILE_CELLS = TILE * TILE;  // 4096 LDS words = 16 KB
+constexpr int UPD_THREADS = 256;
+// per-cell LDS word during one tile:
+//   W_NONE            untouched
+//   W_FREE            freed by >= 1 beam, hit by none
+//   h | FF_BIT * f    hit; h = first hitting beam (< 65536); f = freed by some beam b < h first
+constexpr unsigned W_NONE = 0xFFFFFFFFu;
+constexpr unsigned W_FREE = 0xFFFFFFFEu;
+constexpr unsigned FF_BIT = 0x10000u;
 
 struct RayFrame {
     float mx, my, cs, sn;
@@ -319,7 +330,7 @@ __device__ __forceinline__ RayFrame ray_frame(const LevelGeom &g, const StreamSt
 {
     RayFrame fr;
     float mp[3];
-    map_from_world(g, st.upd_pose, mp);
+    map_from_world(g, st.upd_pose, mp);  // getMapCoordsPose (:124)
     fr.mx = mp[0];
     fr.my = mp[1];
     fr.cs = sdm_cosf(mp[2]);
@@ -327,208 +338,250 @@ __device__ __forceinline__ RayFrame ray_frame(const LevelGeom &g, const StreamSt
     const float f = g.pts_scale;
     float ox = st.origo[0] * f, oy = st.origo[1] * f;
     float nsn = -fr.sn;
-    float bx = fr.mx + (fr.cs * ox + nsn * oy);
+    float bx = fr.mx + (fr.cs * ox + nsn * oy);   // poseTransform * origo (:132)
     float by = fr.my + (fr.sn * ox + fr.cs * oy);
-    fr.bxi = (int)(bx + 0.5f);
+    fr.bxi = (int)(bx + 0.5f);                     // (:135)
     fr.byi = (int)(by + 0.5f);
     return fr;
 }
 
-__device__ __forceinline__ Ray make_ray(const LevelGeom &g, const RayFrame &fr, float2 p)
+__device__ __forceinline__ unsigned make_ray(const LevelGeom &g, const RayFrame &fr, float2 p)
 {
-    Ray r;
-    r.valid = 0;
     const float f = g.pts_scale;
     float px = p.x * f, py = p.y * f;
     float nsn = -fr.sn;
-    float ex = fr.mx + (fr.cs * px + nsn * py);
+    float ex = fr.mx + (fr.cs * px + nsn * py);  // poseTransform * point (:147)
     float ey = fr.my + (fr.sn * px + fr.cs * py);
-    ex += 0.5f;
+    ex += 0.5f;                                   // (:151)
     ey += 0.5f;
-    int x1 = (int)ex, y1 = (int)ey;
+    int x1 = (int)ex, y1 = (int)ey;               // (:154)
     int x0 = fr.bxi, y0 = fr.byi;
-    if (x0 == x1 && y0 == y1) return r;  // :157
-    if ((x0 < 0) || (x0 >= g.sx) || (y0 < 0) || (y0 >= g.sy)) return r;  // :226-229
-    if ((x1 < 0) || (x1 >= g.sx) || (y1 < 0) || (y1 >= g.sy)) return r;  // :235-238
+    if (x0 == x1 && y0 == y1) return RAY_INVALID;
+    if ((x0 < 0) || (x0 >= g.sx) || (y0 < 0) || (y0 >= g.sy)) return RAY_INVALID;
+    if ((x1 < 0) || (x1 >= g.sx) || (y1 < 0) || (y1 >= g.sy)) return RAY_INVALID;
+    return ((unsigned)y1 << 16) | (unsigned)x1;
+}
+
+// Bresenham walk of bresenham2D (:270-299) in closed form: major axis a, minor axis b,
+//   step i in [0, da]:  a(i) = a0 + sa*i,  b(i) = b0 + sb*q(i),  q(i) = floor((e0 + i*db) / da),
+// e0 = da/2 (error_b start, :254/:260).  The incremental error walk keeps error in [0, da), so this
+// is exactly the cell sequence of the reference; steps 0..da-1 are freed, step da is the end cell.
+struct RayWalk {
+    int a0, b0, sa, sb, da, db, e0;
+    bool x_major;
+};
+
+__device__ __forceinline__ RayWalk ray_walk(int x0, int y0, int x1, int y1)
+{
+    RayWalk w;
     int dx = x1 - x0, dy = y1 - y0;
     int adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
-    int odx = dx > 0 ? 1 : -1;           // util::sign (UtilFunctions.h:55-58)
-    int ody = (dy > 0 ? 1 : -1) * g.sx;
-    r.valid = 1;
-    r.start = y0 * g.sx + x0;
-    r.end = y1 * g.sx + x1;
-    if (adx >= ady) {
-        r.abs_da = adx; r.abs_db = ady; r.off_a = odx; r.off_b = ody;
+    int sx = dx > 0 ? 1 : -1, sy = dy > 0 ? 1 : -1;  // util::sign (UtilFunctions.h:55-58)
+    w.x_major = adx >= ady;                         // (:252)
+    if (w.x_major) {
+        w.a0 = x0; w.b0 = y0; w.sa = sx; w.sb = sy; w.da = adx; w.db = ady;
     } else {
-        r.abs_da = ady; r.abs_db = adx; r.off_a = ody; r.off_b = odx;
+        w.a0 = y0; w.b0 = x0; w.sa = sy; w.sb = sx; w.da = ady; w.db = adx;
     }
-    r.e0 = r.abs_da / 2;
-    return r;
+    w.e0 = w.da / 2;
+    return w;
 }
 
-// Marker encoding inside LogOddsCell::upd during one scan (values are resolved before the scan ends;
-// every pre-scan value is <= markFree - 1 because the previous scan left markFree'/markOcc' < markFree):
-//   markFree = U+1                  freed this scan, not hit
-//   H(h)  = hb + (n - h)            hit, first hitting beam h, no earlier free   (hb = U+3)
-//   FH(h) = hb + (n - h) + n + 1    hit by h and freed by some beam b < h
-// atomicMax selects the smallest h; H -> FH conversion is idempotent.
-
-// --------------------------------------------------------------------------- k2: mark hits
-__global__ void __launch_bounds__(256)
-hs_mark_hits_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__restrict__ state,
-                    const float2 *__restrict__ xy, int xy_stride, int stream_begin)
+// Steps [lo, hi] of the walk whose cell lies in the rectangle [A0,A1) x [B0,B1) (major x minor);
+// returns false if none.  q(i) >= Q  <=>  i >= ceil((Q*da - e0)/db);  q(i) <= Q  <=>  i <= floor(((Q+1)*da - e0 - 1)/db).
+__device__ __forceinline__ bool walk_range(const RayWalk &w, int A0, int A1, int B0, int B1, int &lo, int &hi)
 {
-    const int local = blockIdx.z;
+    int ilo, ihi;
+    if (w.sa > 0) {
+        ilo = A0 - w.a0;
+        ihi = A1 - 1 - w.a0;
+    } else {
+        ilo = w.a0 - (A1 - 1);
+        ihi = w.a0 - A0;
+    }
+    lo = ilo > 0 ? ilo : 0;
+    hi = ihi < w.da ? ihi : w.da;
+    if (lo > hi) return false;
+    int qlo, qhi;
+    if (w.sb > 0) {
+        qlo = B0 - w.b0;
+        qhi = B1 - 1 - w.b0;
+    } else {
+        qlo = w.b0 - (B1 - 1);
+        qhi = w.b0 - B0;
+    }
+    if (qhi < 0) return false;
+    if (w.db == 0) {
+        if (qlo > 0) return false;  // q(i) == 0 for every step
+        return true;
+    }
+    if (qlo > 0) {
+        int t = (qlo * w.da - w.e0 + w.db - 1) / w.db;
+        if (t > lo) lo = t;
+    }
+    int t2 = ((qhi + 1) * w.da - w.e0 - 1) / w.db;
+    if (t2 < hi) hi = t2;
+    return lo <= hi;
+}
+
+// ------------------------------------------------------------------- k2: tiled grid update
+// One workgroup per (stream, level).  For each 64x64 tile of the scan's bounding box:
+//   (1) end cells in the tile: LDS atomicMin of the beam index   -> first hitting beam h
+//   (2) free steps in the tile: mark W_FREE, or set FF_BIT on a hit cell when b < h
+//   (3) one coalesced read-modify-write of every touched cell (8 B) applying the reference's
+//       float sequence: free only: l + lf; hit: ((l + lf) - lf) if freed first, then + lo if < 50.
+// This equals running bresenhamCellFree / bresenhamCellOcc (:302-330) beam by beam.
+__global__ void __launch_bounds__(UPD_THREADS)
+hs_update_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__restrict__ state,
+                 const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned smem[];
+    unsigned *tile_w = smem;                 // TILE_CELLS words
+    unsigned *rays = smem + TILE_CELLS;      // max_points packed end cells
+    __shared__ int s_bbox[4];
+    __shared__ int s_any;
+
+    // level-major block order: every stream's level 0 (the largest) is dispatched first
+    const int lvl = blockIdx.x / count;
+    const int local = blockIdx.x - lvl * count;
     const int s = stream_begin + local;
     const StreamState &st = state[s];
     if (!st.do_update) return;
-    const int lvl = blockIdx.y;
     const LevelGeom &g = geom.lv[lvl];
     const int n = st.n;
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.x * 256 >= n) return;
-    LogOddsCell *lc = cells + (size_t)s * geom.stream_cells + g.cell_offset;
-    const RayFrame fr = ray_frame(g, st);
-    unsigned long long L = 0;
-    if (b < n) {
-        Ray r = make_ray(g, fr, xy[(size_t)local * xy_stride + b]);
-        if (r.valid) {
-            const int hb = st.mark_base + 3;
-            atomicMax(&lc[r.end].upd, hb + (n - b));
-            L = (unsigned long long)r.abs_da + 1ull;
-        }
-    }
-    // Σ(abs_da+1): wave reduce, one atomic per wave
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
-    if ((threadIdx.x & 63) == 0 && L) atomicAdd(&state[s].step_cells, L);
-}
-
-// --------------------------------------------------------------------------- k3: free cells
-__global__ void __launch_bounds__(256)
-hs_free_cells_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__restrict__ state,
-                     const float2 *__restrict__ xy, int xy_stride, int stream_begin)
-{
-    __shared__ int s_pref[FREE_BEAMS + 1];
-    __shared__ int s_start[FREE_BEAMS], s_offa[FREE_BEAMS], s_offb[FREE_BEAMS], s_da[FREE_BEAMS],
-        s_db[FREE_BEAMS], s_e0[FREE_BEAMS];
-    const int local = blockIdx.z;
-    const int s = stream_begin + local;
-    const StreamState &st = state[s];
-    if (!st.do_update) return;
-    const int n = st.n;
-    const int b0 = blockIdx.x * FREE_BEAMS;
-    if (b0 >= n) return;
-    const int lvl = blockIdx.y;
-    const LevelGeom &g = geom.lv[lvl];
-    LogOddsCell *lc = cells + (size_t)s * geom.stream_cells + g.cell_offset;
     const int tid = threadIdx.x;
-    if (tid < FREE_BEAMS) {
-        const RayFrame fr = ray_frame(g, st);
-        const int b = b0 + tid;
-        int len = 0;
-        if (b < n) {
-            Ray r = make_ray(g, fr, xy[(size_t)local * xy_stride + b]);
-            if (r.valid) {
-                len = r.abs_da;  // start cell + abs_da-1 intermediate cells are freed (:277-298)
-                s_start[tid] = r.start;
-                s_offa[tid] = r.off_a;
-                s_offb[tid] = r.off_b;
-                s_da[tid] = r.abs_da;
-                s_db[tid] = r.abs_db;
-                s_e0[tid] = r.e0;
-            }
-        }
-        // inclusive scan over the 64 lengths (one wave)
-        int v = len;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            int t = __shfl_up(v, off, 64);
-            if (tid >= off) v += t;
-        }
-        s_pref[tid + 1] = v;
-        if (tid == 0) s_pref[0] = 0;
+    LogOddsCell *lc = cells + (size_t)s * geom.stream_cells + g.cell_offset;
+
+    const RayFrame fr = ray_frame(g, st);
+    const int x0 = fr.bxi, y0 = fr.byi;
+    if (tid == 0) {
+        s_bbox[0] = x0; s_bbox[1] = y0; s_bbox[2] = x0; s_bbox[3] = y0;
+        s_any = 0;
     }
     __syncthreads();
-    const int total = s_pref[FREE_BEAMS];
-    const int mark_free = st.mark_base + 1;
-    const int hb = st.mark_base + 3;
-    const float lf = geom.lf;
-    for (int k = tid; k < total; k += 256) {
-        // beam j: largest j with s_pref[j] <= k
-        int lo = 0, hi = FREE_BEAMS;
+    int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
+    unsigned long long L = 0, R = 0;
+    const float2 *pts = xy + (size_t)local * xy_stride;
+    for (int b = tid; b < n; b += UPD_THREADS) {
+        unsigned r = make_ray(g, fr, pts[b]);
+        rays[b] = r;
+        if (r != RAY_INVALID) {
+            int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+            bx0 = min(bx0, x1); by0 = min(by0, y1); bx1 = max(bx1, x1); by1 = max(by1, y1);
+            int adx = abs(x1 - x0), ady = abs(y1 - y0);
+            L += (unsigned long long)(max(adx, ady) + 1);
+            R += 1;
+        }
+    }
+    if (R) {
+        atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
+        atomicMax(&s_bbox[2], bx1); atomicMax(&s_bbox[3], by1);
+    }
 #pragma unroll
-        for (int it = 0; it < 6; ++it) {
-            int mid = (lo + hi) >> 1;
-            if (s_pref[mid] <= k) lo = mid;
-            else hi = mid;
-        }
-        const int j = lo;
-        const int i = k - s_pref[j];
-        const unsigned int da = (unsigned int)s_da[j];
-        const unsigned int steps_b = ((unsigned int)s_e0[j] + (unsigned int)i * (unsigned int)s_db[j]) / da;
-        const int c = s_start[j] + i * s_offa[j] + (int)steps_b * s_offb[j];
-        const int b = b0 + j;
-        int *updp = &lc[c].upd;
-        int u = __builtin_nontemporal_load(updp) ;
-        if (u < mark_free) {
-            const int old = atomicMax(updp, mark_free);
-            if (old < mark_free) {
-                // first touch this scan: updateSetFree (GridMapLogOdds.h:120-124), unique writer
-                lc[c].l = lc[c].l + lf;
-                continue;
+    for (int off = 32; off >= 1; off >>= 1) {
+        L += __shfl_xor(L, off, 64);
+        R += __shfl_xor(R, off, 64);
+    }
+    if ((tid & 63) == 0 && R) {
+        atomicAdd(&state[s].step_cells, L);
+        atomicAdd(&state[s].tot_cells, L);
+        atomicAdd(&state[s].tot_rays, R);
+    }
+    if (!__syncthreads_or(R != 0)) return;  // no ray drawn on this level
+    const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / TILE;
+    const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / TILE;
+    const int mark_free = st.mark_base + 1;  // currMarkFreeIndex (:120)
+    const int mark_occ = st.mark_base + 2;   // currMarkOccIndex  (:121)
+    const float lf = geom.lf, lo = geom.lo;
+
+    for (int ty = ty0; ty <= ty1; ++ty) {
+        for (int tx = tx0; tx <= tx1; ++tx) {
+            const int X0 = tx * TILE, Y0 = ty * TILE;
+            const int X1 = X0 + TILE, Y1 = Y0 + TILE;
+            // clear the tile words
+            for (int k = tid; k < TILE_CELLS / 4; k += UPD_THREADS)
+                reinterpret_cast<uint4 *>(tile_w)[k] = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
+            __syncthreads();
+            // (1) hits
+            bool any = false;
+            for (int b = tid; b < n; b += UPD_THREADS) {
+                unsigned r = rays[b];
+                if (r == RAY_INVALID) continue;
+                int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+                if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {
+                    atomicMin(&tile_w[(y1 - Y0) * TILE + (x1 - X0)], (unsigned)b);
+                    any = true;
+                }
             }
-            u = old;
-        }
-        if (u > hb && u <= hb + n) {
-            const int h = n - (u - hb);
-            if (b < h) atomicMax(updp, u + n + 1);  // H(h) -> FH(h): freed before the first hit
+            __syncthreads();
+            // (2) free steps
+            for (int b = tid; b < n; b += UPD_THREADS) {
+                unsigned r = rays[b];
+                if (r == RAY_INVALID) continue;
+                int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+                if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
+                RayWalk w = ray_walk(x0, y0, x1, y1);
+                int lo_i, hi_i;
+                bool hit = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i) : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
+                if (!hit) continue;
+                if (hi_i > w.da - 1) hi_i = w.da - 1;  // free steps only
+                if (lo_i > hi_i) continue;
+                any = true;
+                const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
+                int q = (int)(num / (unsigned)w.da);
+                int err = (int)(num - (unsigned)q * (unsigned)w.da);
+                int a = w.a0 + w.sa * lo_i;
+                int bb = w.b0 + w.sb * q;
+                for (int i = lo_i; i <= hi_i; ++i) {
+                    int cx = w.x_major ? a : bb;
+                    int cy = w.x_major ? bb : a;
+                    unsigned *wp = &tile_w[(cy - Y0) * TILE + (cx - X0)];
+                    unsigned v = *wp;
+                    if (v >= W_FREE) {
+                        *wp = W_FREE;
+                    } else if ((unsigned)b < (v & 0xFFFFu)) {
+                        *wp = v | FF_BIT;  // freed by an earlier beam than the first hit
+                    }
+                    a += w.sa;
+                    err += w.db;
+                    if (err >= w.da) {
+                        err -= w.da;
+                        bb += w.sb;
+                    }
+                }
+            }
+            if (any) s_any = 1;
+            __syncthreads();
+            if (s_any) {
+                // (3) apply: wave w handles rows w, w+4, ...; lane = column -> 512 B coalesced rows
+                const int col = tid & 63;
+                const int gx = X0 + col;
+                for (int row = tid >> 6; row < TILE; row += UPD_THREADS / 64) {
+                    const int gy = Y0 + row;
+                    unsigned v = tile_w[row * TILE + col];
+                    if (v == W_NONE || gx >= g.sx || gy >= g.sy) continue;
+                    LogOddsCell *cp = lc + (size_t)gy * g.sx + gx;
+                    LogOddsCell c = *cp;
+                    if (v == W_FREE) {
+                        c.l = c.l + lf;        // updateSetFree (GridMapLogOdds.h:120-124)
+                        c.upd = mark_free;
+                    } else {
+                        if (v & FF_BIT) {
+                            c.l = c.l + lf;    // bresenhamCellFree by an earlier beam
+                            c.l = c.l - lf;    // updateUnsetFree (GridMapLogOdds.h:126-129)
+                        }
+                        if (c.l < 50.0f) c.l = c.l + lo;  // updateSetOccupied (:108-114)
+                        c.upd = mark_occ;
+                    }
+                    *cp = c;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) s_any = 0;
         }
     }
 }
 
-// --------------------------------------------------------------------------- k4: resolve hits
-__global__ void __launch_bounds__(256)
-hs_resolve_hits_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__restrict__ state,
-                       const float2 *__restrict__ xy, int xy_stride, int stream_begin)
-{
-    const int local = blockIdx.z;
-    const int s = stream_begin + local;
-    const StreamState &st = state[s];
-    if (!st.do_update) return;
-    const int n = st.n;
-    if (blockIdx.x * 256 >= n) return;
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= n) return;
-    const int lvl = blockIdx.y;
-    const LevelGeom &g = geom.lv[lvl];
-    LogOddsCell *lc = cells + (size_t)s * geom.stream_cells + g.cell_offset;
-    const RayFrame fr = ray_frame(g, st);
-    Ray r = make_ray(g, fr, xy[(size_t)local * xy_stride + b]);
-    if (!r.valid) return;
-    const int hb = st.mark_base + 3;
-    const int mark_occ = st.mark_base + 2;
-    const int u = lc[r.end].upd;
-    int h;
-    bool freed_first;
-    if (u > hb + n) {
-        h = n - (u - hb - n - 1);
-        freed_first = true;
-    } else {
-        h = n - (u - hb);
-        freed_first = false;
-    }
-    if (h != b) return;
-    // bresenhamCellOcc  H/map/OccGridMapBase.h:315-330
-    float l = lc[r.end].l;
-    if (freed_first) {
-        l = l + geom.lf;   // updateSetFree by the earlier beam
-        l = l - geom.lf;   // updateUnsetFree (GridMapLogOdds.h:126-129)
-    }
-    if (l < 50.0f) l = l + geom.lo;  // updateSetOccupied (GridMapLogOdds.h:108-114)
-    lc[r.end].l = l;
-    lc[r.end].upd = mark_occ;
-}
 
 // --------------------------------------------------------------------------- utility kernels
 __global__ void hs_fill_cells_kernel(LogOddsCell *__restrict__ cells, size_t n)

@@ -51,6 +51,7 @@ def _declare(L):
     L.hs_set_map.argtypes = [_p, _i, _i, _p, _p]
     L.hs_step_batch_device.argtypes = [_p, _i, _i, _p, _i, _p, _p, _p, _p]
     L.hs_get_poses.argtypes = [_p, _p, _p, _p, _p]
+    L.hs_get_counters.argtypes = [_p, _p, _i]
     L.hs_get_device_buffers.argtypes = [_p, P(_p), P(C.c_size_t), P(C.c_size_t)]
     L.hs_get_stream.restype = _p
     L.hs_get_stream.argtypes = [_p]

@@ -198,6 +198,11 @@ class HectorFleet:
         check(self.L.hs_get_poses(self.h, _fp(p), _fp(cv), _fp(d), _fp(cells)), "hs_get_poses")
         return p, cv.reshape(self.B, 3, 3), d.astype(bool), cells
 
+    def counters(self, reset=True):
+        o = np.zeros(5, np.int64)
+        check(self.L.hs_get_counters(self.h, _fp(o), 1 if reset else 0), "hs_get_counters")
+        return {"cells": int(o[0]), "rays": int(o[1]), "gn_points": int(o[2]), "updates": int(o[3]), "steps": int(o[4])}
+
     def stream_handle(self) -> int:
         return int(self.L.hs_get_stream(self.h) or 0)
 
@@ -205,10 +210,10 @@ class HectorFleet:
         check(self.L.hs_set_timing(self.h, 1 if enable else 0), "hs_set_timing")
 
     def kernel_times(self, reset=True):
-        ms = np.zeros(4, np.float64)
-        n = np.zeros(4, np.int64)
+        ms = np.zeros(2, np.float64)
+        n = np.zeros(2, np.int64)
         check(self.L.hs_get_kernel_times(self.h, _fp(ms), _fp(n), 1 if reset else 0), "hs_get_kernel_times")
-        names = ("match", "mark_hits", "free_cells", "resolve_hits")
+        names = ("match", "update")
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}
 
 

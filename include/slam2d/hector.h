@@ -47,6 +47,7 @@ const char *hs_last_error(void);
 /* HectorSlamProcessor ctor + MapRepMultiMap ctor (HectorSlamProcessor.h:57-68, MapRepMultiMap.h:57-90).
  * map_resolution/map_size/start/levels are the ROS params map_resolution, map_size, map_start_x/y,
  * map_multi_res_levels (hector_slam.cc:138-142).  max_points bounds the scan size (>= 1). */
+/* Limits: map sizes <= 32768 cells per side, 1 <= max_points <= 65535. */
 int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_x, int map_size_y,
               float map_start_x, float map_start_y, int levels, int max_points);
 /* ~HectorSlamProcessor (HectorSlamProcessor.h:70-73) */
@@ -100,6 +101,10 @@ int hs_step_batch_device(hs_ctx *ctx, int stream_begin, int count, const float *
 /* Copy poses (float3), covariances (float9), did-update flags and Σ cells traversed of the last
  * step (int64, Σ_levels Σ_valid rays (abs_da + 1)) for every stream.  Any pointer may be NULL. */
 int hs_get_poses(hs_ctx *ctx, float *poses_out, float *covs_out, int *did_update_out, int64_t *cells_traversed_out);
+/* Cumulative work counters summed over streams since the last reset (synchronises):
+ * out[0] Σ cells traversed (Σ abs_da+1), out[1] valid rays, out[2] Σ points x GN iterations,
+ * out[3] map updates, out[4] steps.  reset != 0 zeroes them afterwards. */
+int hs_get_counters(hs_ctx *ctx, int64_t out[5], int reset);
 /* Device pointer of the per-stream state array and of the cell storage (for zero-copy consumers). */
 int hs_get_device_buffers(hs_ctx *ctx, void **cells, size_t *cells_bytes, size_t *stream_cells);
 /* The context's own HIP stream (hipStream_t as void*). */
@@ -107,10 +112,10 @@ void *hs_get_stream(hs_ctx *ctx);
 
 /* ---- measurement ----------------------------------------------------------------------------- */
 /* Kernel timing with HIP events recorded on the launch stream around every kernel of every step
- * (enable = 1).  hs_get_kernel_times fills, for the 4 kernels {match, mark_hits, free_cells,
- * resolve_hits}, the accumulated milliseconds and launch counts since the last reset (synchronises). */
+ * (enable = 1).  hs_get_kernel_times fills, for the 2 kernels {hs_match_kernel, hs_update_kernel},
+ * the accumulated milliseconds and launch counts since the last reset (synchronises). */
 int hs_set_timing(hs_ctx *ctx, int enable);
-int hs_get_kernel_times(hs_ctx *ctx, double ms_out[4], int64_t launches_out[4], int reset);
+int hs_get_kernel_times(hs_ctx *ctx, double ms_out[2], int64_t launches_out[2], int reset);
 
 #ifdef __cplusplus
 }

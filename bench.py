@@ -39,7 +39,7 @@ CONFIGS = {
     # BASELINE configs[2]: 3-level 4096^2
     "c3": dict(map_size=4096, levels=3, streams=256),
 }
-KERNELS = ("match", "update")
+KERNELS = ("match", "bin", "tile")
 
 
 def log(*a):
@@ -52,7 +52,9 @@ def algorithmic_bytes(ctr: dict, levels: int) -> dict:
     B_update = ΣL 16 B (8 B LogOddsCell read + 8 B write per traversed cell, ΣL = Σ (abs_da+1))."""
     b_match = ctr["gn_points"] * 24
     b_update = ctr["cells"] * 16
-    return {"match": b_match, "update": b_update, "total": b_match + b_update,
+    # hs_bin_kernel: reads every level's points (8 B) and writes the packed end cell (4 B) per ray
+    b_bin = ctr["rays"] * 12
+    return {"match": b_match, "bin": b_bin, "tile": b_update, "total": b_match + b_update,
             "read_only": b_match + ctr["cells"] * 8}
 
 
@@ -79,32 +81,33 @@ def cpu_baseline(cfg, seconds=10.0, max_scans=4000):
                       f"{cfg['levels']} levels, forced map update, oracle/hector_oracle.c -O2 single thread"}
 
 
-def pose_check(cfg, n_scans=40):
-    """Pose error of the GPU path vs the oracle in the reference's sequential summation order
-    (the metric's 'pose RMSE vs ref'), one stream, forced updates."""
+def pose_check(cfg, S, gpu_poses):
+    """Pose error of the benchmarked GPU streams (device pose log, every step incl. warmup) vs the
+    CPU oracle in the reference's sequential summation order on the same scans -- the metric's
+    'pose RMSE vs ref' -- plus the absolute error against the synthetic ground truth."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
-    from slam2d import synth
-    from slam2d.hector import HectorFleet
 
-    S = synth.make_streams(1, n_scans, seed=4242)
-    f = HectorFleet(1, 0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], max_points=1081)
-    r = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0)
-    for x in (f, r):
-        x.set_update_factors(0.4, 0.9)
-        x.set_thresholds(-1.0, -1.0)
-    e = []
-    for k in range(n_scans):
-        pts = S.points[0, k, : S.counts[0, k]]
-        gp, _, _ = f.update(0, pts)
-        rp, _, _ = r.process(pts)
-        e.append(gp.astype(np.float64) - rp.astype(np.float64))
-    f.close()
-    e = np.asarray(e)
-    return {"scans": n_scans, "rmse_xy_m": float(np.sqrt(np.mean(e[:, 0] ** 2 + e[:, 1] ** 2))),
+    n_streams, n_scans = gpu_poses.shape[1], gpu_poses.shape[0]
+    e, egt = [], []
+    for s in range(n_streams):
+        r = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0)
+        r.set_update_factors(0.4, 0.9)
+        r.set_thresholds(-1.0, -1.0)
+        for k in range(n_scans):
+            rp, _, _ = r.process(S.points[s, k, : S.counts[s, k]])
+            e.append(gpu_poses[k, s].astype(np.float64) - rp.astype(np.float64))
+            egt.append(gpu_poses[k, s].astype(np.float64) - S.gt[s, k])
+        r.close()
+    e, egt = np.asarray(e), np.asarray(egt)
+    egt[:, 2] = np.arctan2(np.sin(egt[:, 2]), np.cos(egt[:, 2]))
+    return {"streams": n_streams, "scans_per_stream": n_scans,
+            "rmse_xy_m": float(np.sqrt(np.mean(e[:, 0] ** 2 + e[:, 1] ** 2))),
             "rmse_theta_rad": float(np.sqrt(np.mean(e[:, 2] ** 2))),
             "max_abs_xy_m": float(np.abs(e[:, :2]).max()), "max_abs_theta_rad": float(np.abs(e[:, 2]).max()),
-            "tolerance": "1e-4 m / 1e-4 rad (north_star)"}
+            "tolerance": "1e-4 m / 1e-4 rad (north_star)",
+            "vs_ground_truth_rmse_xy_m": float(np.sqrt(np.mean(egt[:, 0] ** 2 + egt[:, 1] ** 2))),
+            "vs_ground_truth_rmse_theta_rad": float(np.sqrt(np.mean(egt[:, 2] ** 2)))}
 
 
 def main():
@@ -152,6 +155,9 @@ def main():
     fleet.set_update_factors(0.4, 0.9)   # hector_slam.cc:144-145
     fleet.set_thresholds(-1.0, -1.0)     # benchmark mode: update every scan
     hs = torch.cuda.current_stream(dev).cuda_stream
+    n_log = min(2, B)
+    d_plog = torch.zeros((T, n_log, 3), dtype=torch.float32, device=dev)
+    fleet.set_pose_log(d_plog.data_ptr(), n_log, T)
     stride = pts.shape[2]
     step_bytes = pts.shape[1] * pts.shape[2] * 8
 
@@ -191,7 +197,7 @@ def main():
     if rank == 0:
         ab = algorithmic_bytes(ctr, cfg["levels"])
         roof = None
-        if not args.no_timing and ktimes["update"][1] > 0:
+        if not args.no_timing and ktimes["tile"][1] > 0:
             dom = max(KERNELS, key=lambda k: ktimes[k][0])
             ms, nlaunch = ktimes[dom]
             per_launch_bytes = ab[dom] / nlaunch
@@ -210,7 +216,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg)
-        pose = pose_check(cfg) if world == 1 else None
+        pose = pose_check(cfg, S, d_plog.cpu().numpy())
         out = {"metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K,
                "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",

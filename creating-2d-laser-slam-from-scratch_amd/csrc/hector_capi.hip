@@ -7,6 +7,7 @@
 #include <float.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -36,7 +37,7 @@ int fail(int code, const char *what, hipError_t e = hipSuccess)
         if (_e != hipSuccess) return fail(HS_EHIP, #expr, _e); \
     } while (0)
 
-constexpr int NKERN = 2;
+constexpr int NKERN = 3;
 
 struct EventPair {
     hipEvent_t a, b;
@@ -48,7 +49,7 @@ struct hs_ctx {
     int B = 0, levels = 0, max_points = 0, sx = 0, sy = 0;
     float res = 0, start_x = 0, start_y = 0;
     FleetGeom geom{};
-    LogOddsCell *d_cells = nullptr;
+    float *d_cells = nullptr;  // tiled words (hector_internal.h)
     size_t cells_bytes = 0;
     StreamState *d_state = nullptr;
     // single-stream staging (host-pointer entry points)
@@ -59,12 +60,21 @@ struct hs_ctx {
     float *d_out_pose = nullptr;
     float *d_out_cov = nullptr;
     int8_t *d_occ = nullptr;
+    PoseLog plog{nullptr, 0, 0};
     hipStream_t stream = nullptr;
     // timing
     bool timing = false;
     std::vector<EventPair> ev_used, ev_free;
-    double acc_ms[NKERN] = {0, 0};
-    int64_t acc_n[NKERN] = {0, 0};
+    double acc_ms[NKERN] = {0, 0, 0};
+    int64_t acc_n[NKERN] = {0, 0, 0};
+    // binned grid update scratch
+    unsigned *d_rays = nullptr;
+    uint4 *d_segs = nullptr;
+    WorkItem *d_items = nullptr;
+    WorkItem *d_wholes = nullptr;
+    WorkQueue *d_wq = nullptr;
+    unsigned seg_cap = 0, item_cap = 0;
+    int tile_grid = 0;
 };
 
 namespace {
@@ -101,13 +111,15 @@ void init_geometry(hs_ctx *c)
         L.inv_t[0] = (-L.inv_l[0]) * L.map_t[0] + (-L.inv_l[1]) * L.map_t[1];
         L.inv_t[1] = (-L.inv_l[2]) * L.map_t[0] + (-L.inv_l[3]) * L.map_t[1];
         L.pts_scale = (float)(1.0 / pow(2.0, (double)i));
-        L.cell_offset = off;
-        off += (size_t)rx * (size_t)ry;
+        L.tiles_x = (rx + TILE - 1) / TILE;
+        L.tiles_y = (ry + TILE_H - 1) / TILE_H;
+        L.word_offset = off;
+        off += (size_t)L.tiles_x * L.tiles_y * TILE_BLOCK_WORDS;
         rx /= 2;
         ry /= 2;
         res *= 2.0f;
     }
-    g.stream_cells = off;
+    g.stream_words = off;
 }
 
 // GridMapLogOddsFunctions::probToLogOdds  GridMapLogOdds.h:153-157
@@ -130,8 +142,8 @@ StreamState initial_state()
 
 int reset_all(hs_ctx *c)
 {
-    size_t ncell = c->cells_bytes / sizeof(LogOddsCell);
-    hipLaunchKernelGGL(hs_fill_cells_kernel, dim3(4096), dim3(256), 0, c->stream, c->d_cells, ncell);
+    size_t nwords = c->cells_bytes / sizeof(float);
+    hipLaunchKernelGGL(hs_fill_cells_kernel, dim3(4096), dim3(256), 0, c->stream, c->d_cells, nwords);
     HCHK(hipGetLastError());
     std::vector<StreamState> h(c->B, initial_state());
     HCHK(hipMemcpyAsync(c->d_state, h.data(), sizeof(StreamState) * c->B, hipMemcpyHostToDevice, c->stream));
@@ -167,14 +179,18 @@ int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride
     if (count <= 0) return HS_OK;
     begin_timed(c, 0, s);
     hipLaunchKernelGGL(hs_match_kernel, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state, xy,
-                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov);
+                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, c->d_wq);
     end_timed(c, s);
     HCHK(hipGetLastError());
     if (mode == MODE_MATCH_ONLY) return HS_OK;
-    const size_t shmem = sizeof(unsigned) * ((size_t)TILE_CELLS + (size_t)c->max_points);
     begin_timed(c, 1, s);
-    hipLaunchKernelGGL(hs_update_kernel, dim3(count * c->levels), dim3(UPD_THREADS), shmem, s, c->geom, c->d_cells,
-                       c->d_state, xy, xy_stride, begin, count, c->max_points);
+    hipLaunchKernelGGL(hs_bin_kernel, dim3(count), dim3(BIN_THREADS), 0, s, c->geom, c->d_state, xy, xy_stride, begin,
+                       c->max_points, c->d_rays, c->d_segs, c->d_items, c->d_wholes, c->d_wq, c->seg_cap, c->item_cap);
+    end_timed(c, s);
+    HCHK(hipGetLastError());
+    begin_timed(c, 2, s);
+    hipLaunchKernelGGL(hs_tile_kernel, dim3(c->tile_grid), dim3(TILE_THREADS), 0, s, c->geom, c->d_cells, c->d_state,
+                       c->d_rays, c->d_segs, c->d_items, c->d_wholes, c->d_wq, c->max_points);
     end_timed(c, s);
     HCHK(hipGetLastError());
     return HS_OK;
@@ -227,7 +243,7 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
     c->geom.lo = prob_to_logodds(0.6f);
     c->geom.min_dist = 0.4f * 1.0f;      // HectorSlamProcessor ctor (HectorSlamProcessor.h:66-67)
     c->geom.min_ang = 0.13f * 1.0f;
-    c->cells_bytes = sizeof(LogOddsCell) * c->geom.stream_cells * (size_t)num_streams;
+    c->cells_bytes = sizeof(float) * c->geom.stream_words * (size_t)num_streams;
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
@@ -244,6 +260,46 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         (e = hipMalloc(&c->d_occ, (size_t)map_size_x * map_size_y)) != hipSuccess) {
         hs_destroy(c);
         return fail(HS_ENOMEM, "hipMalloc", e);
+    }
+    {
+        // grid-update queues: 6 segments per ray on average, 512 non-empty tiles per stream level
+        const size_t sl = (size_t)num_streams * levels;
+        size_t segs = sl * (size_t)max_points * 6, its = sl * 512;
+        if (segs < (1u << 20)) segs = 1u << 20;
+        if (its < (1u << 14)) its = 1u << 14;
+        // test hook: shrink the queues to exercise the WHOLE (unbinned) fallback
+        if (const char *e = getenv("SLAM2D_SEG_CAP")) segs = (size_t)atoll(e);
+        if (const char *e = getenv("SLAM2D_ITEM_CAP")) its = (size_t)atoll(e);
+        c->seg_cap = (unsigned)(segs < 0xFFFFFFF0ull ? segs : 0xFFFFFFF0ull);
+        c->item_cap = (unsigned)(its < 0xFFFFFFF0ull ? its : 0xFFFFFFF0ull);
+        int dev = 0, ncu = 256;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        // grid-stride tile kernel: exactly the resident workgroups (occupancy query), overridable
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hs_tile_kernel, TILE_THREADS, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 4;
+        const char *tg = getenv("SLAM2D_TILE_WG_PER_CU");
+        c->tile_grid = ncu * (tg ? atoi(tg) : per_cu);
+    }
+    if ((e = hipMalloc(&c->d_rays, sizeof(unsigned) * (size_t)num_streams * levels * max_points)) != hipSuccess ||
+        (e = hipMalloc(&c->d_segs, sizeof(uint4) * (size_t)c->seg_cap)) != hipSuccess ||
+        (e = hipMalloc(&c->d_items, sizeof(WorkItem) * (size_t)c->item_cap)) != hipSuccess ||
+        (e = hipMalloc(&c->d_wholes, sizeof(WorkItem) * (size_t)num_streams * levels)) != hipSuccess ||
+        (e = hipMalloc(&c->d_wq, sizeof(WorkQueue))) != hipSuccess) {
+        hs_destroy(c);
+        return fail(HS_ENOMEM, "hipMalloc", e);
+    }
+    {
+        WorkQueue q;
+        memset(&q, 0, sizeof(q));
+        q.item_cap = c->item_cap;
+        q.seg_cap = c->seg_cap;
+        if ((e = hipMemcpy(c->d_wq, &q, sizeof(q), hipMemcpyHostToDevice)) != hipSuccess) {
+            hs_destroy(c);
+            return fail(HS_EHIP, "hipMemcpy(work queue)", e);
+        }
     }
     int rc = reset_all(c);
     if (rc != HS_OK) {
@@ -267,6 +323,11 @@ int hs_destroy(hs_ctx *c)
     hipFree(c->d_out_pose);
     hipFree(c->d_out_cov);
     hipFree(c->d_occ);
+    hipFree(c->d_rays);
+    hipFree(c->d_segs);
+    hipFree(c->d_items);
+    hipFree(c->d_wholes);
+    hipFree(c->d_wq);
     for (auto &p : c->ev_used) {
         hipEventDestroy(p.a);
         hipEventDestroy(p.b);
@@ -396,23 +457,28 @@ int hs_get_map(hs_ctx *c, int stream, int level, int8_t *occ_out, float *logodds
     if (check_stream(c, stream) != HS_OK || level < 0 || level >= c->levels) return fail(HS_EINVAL, "bad stream/level");
     const LevelGeom &L = c->geom.lv[level];
     const size_t ncell = (size_t)L.sx * L.sy;
-    const LogOddsCell *base = c->d_cells + (size_t)stream * c->geom.stream_cells + L.cell_offset;
+    const size_t nwords = (size_t)L.tiles_x * L.tiles_y * TILE_BLOCK_WORDS;
+    const float *base = c->d_cells + (size_t)stream * c->geom.stream_words + L.word_offset;
     if (occ_out) {
-        hipLaunchKernelGGL(hs_publish_kernel, dim3(1024), dim3(256), 0, c->stream, base, c->d_occ, ncell);
+        hipLaunchKernelGGL(hs_publish_kernel, dim3(1024), dim3(256), 0, c->stream, base, L, c->d_occ);
         HCHK(hipGetLastError());
         HCHK(hipMemcpyAsync(occ_out, c->d_occ, ncell, hipMemcpyDeviceToHost, c->stream));
     }
-    std::vector<LogOddsCell> tmp;
+    std::vector<float> tmp;
     if (logodds_out || upd_out) {
-        tmp.resize(ncell);
-        HCHK(hipMemcpyAsync(tmp.data(), base, sizeof(LogOddsCell) * ncell, hipMemcpyDeviceToHost, c->stream));
+        tmp.resize(nwords);
+        HCHK(hipMemcpyAsync(tmp.data(), base, sizeof(float) * nwords, hipMemcpyDeviceToHost, c->stream));
     }
     StreamState st;
     HCHK(hipMemcpyAsync(&st, c->d_state + stream, sizeof(st), hipMemcpyDeviceToHost, c->stream));
     HCHK(hipStreamSynchronize(c->stream));
-    for (size_t i = 0; i < tmp.size(); ++i) {
-        if (logodds_out) logodds_out[i] = tmp[i].l;
-        if (upd_out) upd_out[i] = tmp[i].upd;
+    if (!tmp.empty()) {
+        for (int y = 0; y < L.sy; ++y)
+            for (int x = 0; x < L.sx; ++x) {
+                const size_t w = cell_word(L, x, y), o = (size_t)y * L.sx + x;
+                if (logodds_out) logodds_out[o] = tmp[w];
+                if (upd_out) memcpy(&upd_out[o], &tmp[w + TILE_CELLS], sizeof(int32_t));
+            }
     }
     if (update_index_out) *update_index_out = st.map_updates - 1;
     return HS_OK;
@@ -423,14 +489,18 @@ int hs_set_map(hs_ctx *c, int stream, int level, const float *logodds, const int
     if (check_stream(c, stream) != HS_OK || level < 0 || level >= c->levels || !logodds || !upd)
         return fail(HS_EINVAL, "bad arguments");
     const LevelGeom &L = c->geom.lv[level];
-    const size_t ncell = (size_t)L.sx * L.sy;
-    std::vector<LogOddsCell> tmp(ncell);
-    for (size_t i = 0; i < ncell; ++i) {
-        tmp[i].l = logodds[i];
-        tmp[i].upd = upd[i];
-    }
-    LogOddsCell *base = c->d_cells + (size_t)stream * c->geom.stream_cells + L.cell_offset;
-    HCHK(hipMemcpyAsync(base, tmp.data(), sizeof(LogOddsCell) * ncell, hipMemcpyHostToDevice, c->stream));
+    const size_t nwords = (size_t)L.tiles_x * L.tiles_y * TILE_BLOCK_WORDS;
+    float *base = c->d_cells + (size_t)stream * c->geom.stream_words + L.word_offset;
+    std::vector<float> tmp(nwords);
+    HCHK(hipMemcpyAsync(tmp.data(), base, sizeof(float) * nwords, hipMemcpyDeviceToHost, c->stream));
+    HCHK(hipStreamSynchronize(c->stream));
+    for (int y = 0; y < L.sy; ++y)
+        for (int x = 0; x < L.sx; ++x) {
+            const size_t w = cell_word(L, x, y), o = (size_t)y * L.sx + x;
+            tmp[w] = logodds[o];
+            memcpy(&tmp[w + TILE_CELLS], &upd[o], sizeof(int32_t));
+        }
+    HCHK(hipMemcpyAsync(base, tmp.data(), sizeof(float) * nwords, hipMemcpyHostToDevice, c->stream));
     HCHK(hipStreamSynchronize(c->stream));
     return HS_OK;
 }
@@ -483,12 +553,41 @@ int hs_get_counters(hs_ctx *c, int64_t out[5], int reset)
     return HS_OK;
 }
 
-int hs_get_device_buffers(hs_ctx *c, void **cells, size_t *cells_bytes, size_t *stream_cells)
+int hs_get_queue_stats(hs_ctx *c, int64_t out[8], int reset_stamps)
+{
+    if (!c || !out) return fail(HS_EINVAL, "NULL argument");
+    WorkQueue q;
+    unsigned long long st[8];
+    HCHK(hipDeviceSynchronize());
+    HCHK(hipMemcpy(&q, c->d_wq, sizeof(q), hipMemcpyDeviceToHost));
+    HCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
+    out[0] = q.item_used;
+    out[1] = q.seg_used;
+    out[2] = q.whole_used;
+    out[3] = q.overflow;
+    for (int k = 0; k < 4; ++k) out[4 + k] = (int64_t)st[k];
+    if (reset_stamps) {
+        memset(st, 0, sizeof(st));
+        HCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), st, sizeof(st)));
+    }
+    return HS_OK;
+}
+
+int hs_get_device_buffers(hs_ctx *c, void **cells, size_t *cells_bytes, size_t *stream_words)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
     if (cells) *cells = c->d_cells;
     if (cells_bytes) *cells_bytes = c->cells_bytes;
-    if (stream_cells) *stream_cells = c->geom.stream_cells;
+    if (stream_words) *stream_words = c->geom.stream_words;
+    return HS_OK;
+}
+
+int hs_set_pose_log(hs_ctx *c, float *d_buf, int streams, int capacity)
+{
+    if (!c || streams < 0 || capacity < 0 || (d_buf && streams > c->B)) return fail(HS_EINVAL, "bad pose log");
+    c->plog.buf = d_buf;
+    c->plog.streams = d_buf ? streams : 0;
+    c->plog.capacity = d_buf ? capacity : 0;
     return HS_OK;
 }
 
@@ -501,7 +600,7 @@ int hs_set_timing(hs_ctx *c, int enable)
     return HS_OK;
 }
 
-int hs_get_kernel_times(hs_ctx *c, double ms_out[2], int64_t launches_out[2], int reset)
+int hs_get_kernel_times(hs_ctx *c, double ms_out[3], int64_t launches_out[3], int reset)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
     for (auto &p : c->ev_used) {

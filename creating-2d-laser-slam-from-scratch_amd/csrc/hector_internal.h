@@ -9,7 +9,16 @@ constexpr double S2D_PI = 3.14159265358979323846;  // M_PI
 constexpr int MAX_LEVELS = 8;
 constexpr int MATCH_THREADS = 256;
 constexpr int MATCH_WAVES = MATCH_THREADS / 64;
-constexpr int FREE_BEAMS = 64;  // beams per free-cells workgroup
+// Cell storage is tiled: a level is a grid of TILE x TILE_H tiles (padded up), each tile one
+// contiguous 16 KB block = 2048 log-odds floats (row-major 32 x 64) followed by the 2048 matching
+// updateIndex ints.  A tile is exactly the unit the grid-update kernel reads and writes.
+#ifndef S2D_TILE_H
+#define S2D_TILE_H 32
+#endif
+constexpr int TILE = 64;
+constexpr int TILE_H = S2D_TILE_H;
+constexpr int TILE_CELLS = TILE * TILE_H;   // 2048 at 64 x 32
+constexpr int TILE_BLOCK_WORDS = 2 * TILE_CELLS;
 
 enum StepMode : int {
     MODE_PROCESS = 0,        // HectorSlamProcessor::update
@@ -18,12 +27,8 @@ enum StepMode : int {
     MODE_UPDATE_ONLY = 3,    // MapRepMultiMap::updateByScan with a given pose
 };
 
-// LogOddsCell (lesson4/include/lesson4/hector_mapping/map/GridMapLogOdds.h:37-87), same 8-byte layout.
-struct LogOddsCell {
-    float l;
-    int upd;
-};
-static_assert(sizeof(LogOddsCell) == 8, "LogOddsCell must be 8 bytes");
+// LogOddsCell (lesson4/include/lesson4/hector_mapping/map/GridMapLogOdds.h:37-87): {logOddsVal,
+// updateIndex}; stored split into the two planes of a tile block (see above).
 
 // One pyramid level: GridMapBase transforms (GridMapBase.h:270-286) + MapDimensionProperties limits.
 struct LevelGeom {
@@ -35,14 +40,24 @@ struct LevelGeom {
     float lim[2];     // mapLimitsf = dims - 2
     float pts_scale;  // DataPointContainer::setFrom factor 1/2^level
     float cell_len;
-    size_t cell_offset;  // offset of this level inside a stream's cell block
+    int tiles_x, tiles_y;  // storage tiles (sx, sy rounded up to TILE, TILE_H)
+    size_t word_offset;    // offset of this level inside a stream's block, in 4-byte words
 };
+
+// word index of cell (x, y)'s log-odds inside its level; its updateIndex is TILE_CELLS words later
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline size_t cell_word(const LevelGeom &g, int x, int y)
+{
+    return ((size_t)((y / TILE_H) * g.tiles_x + (x / TILE)) * TILE_BLOCK_WORDS) + (size_t)((y % TILE_H) * TILE + (x % TILE));
+}
 
 struct FleetGeom {
     int levels;
     float lf, lo;              // logOddsFree / logOddsOccupied
     float min_dist, min_ang;   // map update thresholds
-    size_t stream_cells;       // cells per stream (all levels)
+    size_t stream_words;       // 4-byte words per stream (all levels, tiled, both planes)
     LevelGeom lv[MAX_LEVELS];
 };
 
@@ -66,6 +81,31 @@ struct alignas(16) StreamState {
     unsigned long long tot_gn_points; // Σ over GN iterations of the points evaluated
     unsigned long long tot_updates;   // map updates (steps with do_update)
     unsigned long long tot_steps;     // steps
+    int step_index;                   // steps since hs_reset (pose-log row)
+    int pad_;
+};
+
+// Binned grid-update work queue (hs_bin_kernel -> hs_tile_kernel).
+struct WorkItem {
+    int s;                 // stream
+    int lvl_kind;          // level | kind << 8 (0 = one tile + its segment list, 1 = whole level)
+    unsigned tile_xy;      // first tile (x | y << 16), in tiles
+    unsigned begin_xy;     // ray start cell (x | y << 16)
+    unsigned seg_begin;    // tile: first segment; whole: ntx | nty << 16
+    unsigned seg_count;    // tile: number of segments
+    unsigned mark_base;    // stream's currUpdateIndex for this step (marks = +1 / +2)
+    unsigned n;            // points of the scan (whole items)
+};
+struct WorkQueue {
+    unsigned seg_used, item_used, whole_used, overflow;  // zeroed by hs_match_kernel every step
+    unsigned item_cap, seg_cap, pad_[2];
+};
+
+// Optional device pose log: the match kernel appends every step's pose of streams [0, streams).
+struct PoseLog {
+    float *buf;    // [capacity][streams][3]
+    int streams;
+    int capacity;
 };
 
 }  // namespace s2d

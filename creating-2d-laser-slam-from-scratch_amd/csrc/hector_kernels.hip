@@ -3,8 +3,9 @@
 // abbreviated H/ below).  Host orchestration + C-ABI live in hector_capi.hip.
 //
 // Data layout in HBM (per context):
-//   cells  : LogOddsCell {float l; int upd} (8 B, H/map/GridMapLogOdds.h:37-87), row-major
-//            [stream][level][y][x]; a stream's levels are contiguous (stream_cells per stream).
+//   cells  : LogOddsCell {float l; int upd} (H/map/GridMapLogOdds.h:37-87) stored tiled: per stream,
+//            per level, 64 x 32-cell tiles of 16 KB each = [2048 log-odds floats][2048 updateIndex
+//            ints] (see hector_internal.h cell_word); the tile is the grid update's unit of work.
 //   state  : StreamState per stream (pose, last map-update pose, covariance, update indices).
 //   points : float2 per beam in level-0 map scale, padded to xy_stride per stream.
 //
@@ -100,7 +101,7 @@ __device__ __forceinline__ void solve3(const float *m, const float *b, float *d)
 // Per point: OccGridMapUtil::getCompleteHessianDerivs body (H/map/OccGridMapUtil.h:94-126) with
 // interpMapValueWithDerivatives (:139-228).  Accumulates into acc[9] =
 // {dTr0, dTr1, dTr2, H00, H11, H22, H01, H02, H12}.
-__device__ __forceinline__ void point_terms(const LogOddsCell *__restrict__ cells, const LevelGeom &g, float tx,
+__device__ __forceinline__ void point_terms(const float *__restrict__ lvl_words, const LevelGeom &g, float tx,
                                             float ty, float cs, float sn, float px, float py, float *acc)
 {
     float nsn = -sn;
@@ -115,12 +116,11 @@ __device__ __forceinline__ void point_terms(const LogOddsCell *__restrict__ cell
         int ix = (int)x, iy = (int)y;
         float fx = x - (float)ix;
         float fy = y - (float)iy;
-        const LogOddsCell *c0 = cells + ((size_t)iy * g.sx + ix);
-        const LogOddsCell *c2 = c0 + g.sx;
-        float i0 = cell_prob(c0[0].l);
-        float i1 = cell_prob(c0[1].l);
-        float i2 = cell_prob(c2[0].l);
-        float i3 = cell_prob(c2[1].l);
+        // 4 neighbours (:160-192); ix <= sx-2, iy <= sy-2 by the bounds check
+        float i0 = cell_prob(lvl_words[cell_word(g, ix, iy)]);
+        float i1 = cell_prob(lvl_words[cell_word(g, ix + 1, iy)]);
+        float i2 = cell_prob(lvl_words[cell_word(g, ix, iy + 1)]);
+        float i3 = cell_prob(lvl_words[cell_word(g, ix + 1, iy + 1)]);
         float dx1 = i0 - i1;
         float dx2 = i2 - i3;
         float dy1 = i0 - i2;
@@ -147,7 +147,7 @@ __device__ __forceinline__ void point_terms(const LogOddsCell *__restrict__ cell
 
 // One Gauss-Newton step, ScanMatcher::estimateTransformationLogLh (H/matcher/ScanMatcher.h:107-139).
 // Every thread ends with the same H, b and estimate (xor-butterfly reductions are symmetric).
-__device__ __forceinline__ void gn_step(const LogOddsCell *__restrict__ cells, const LevelGeom &g,
+__device__ __forceinline__ void gn_step(const float *__restrict__ cells, const LevelGeom &g,
                                         const float2 *__restrict__ pts, int n, float f, float *est, float *H,
                                         float (*red)[MATCH_WAVES][9], int parity, int *clamps)
 {
@@ -202,17 +202,17 @@ __device__ __forceinline__ void gn_step(const LogOddsCell *__restrict__ cells, c
 }
 
 __global__ void __launch_bounds__(MATCH_THREADS)
-hs_match_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__restrict__ state,
+hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__restrict__ state,
                 const float2 *__restrict__ xy, int xy_stride, const int *__restrict__ counts,
                 const float2 *__restrict__ origo, const float *__restrict__ hints, int stream_begin, int mode,
-                float *__restrict__ out_pose, float *__restrict__ out_cov)
+                float *__restrict__ out_pose, float *__restrict__ out_cov, PoseLog plog, WorkQueue *__restrict__ wq)
 {
     static_assert(MATCH_THREADS == 64 * MATCH_WAVES && MATCH_WAVES == 4, "reduction tree assumes 4 waves");
     __shared__ float red[2][MATCH_WAVES][9];
     const int local = blockIdx.x;
     const int s = stream_begin + local;
     StreamState &st = state[s];
-    const LogOddsCell *scells = cells + (size_t)s * geom.stream_cells;
+    const float *scells = cells + (size_t)s * geom.stream_words;
     const float2 *pts = xy + (size_t)local * xy_stride;
     const int n = counts[local];
 
@@ -240,7 +240,7 @@ hs_match_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__
             const LevelGeom &g = geom.lv[lvl];
             const int iters = lvl == 0 ? 5 : 3;
             if (n == 0) continue;  // ScanMatcher::matchData returns the hint (ScanMatcher.h:65, :96)
-            const LogOddsCell *lc = scells + g.cell_offset;
+            const float *lc = scells + g.word_offset;
             float est[3], H[9];
             map_from_world(g, tmp, est);
             for (int it = 0; it <= iters; ++it) {
@@ -257,6 +257,11 @@ hs_match_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__
         np_[2] = tmp[2];
     }
     if (threadIdx.x != 0) return;
+    if (local == 0) {  // reset the grid-update work queue for this step (consumed by k2/k3)
+        wq->seg_used = 0;
+        wq->item_used = 0;
+        wq->whole_used = 0;
+    }
 
     if (out_pose) {
         out_pose[3 * local] = np_[0];
@@ -268,6 +273,13 @@ hs_match_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__
     }
     st.clamp_count += clamps;
     st.tot_steps += 1;
+    if (plog.buf && s < plog.streams && st.step_index < plog.capacity) {
+        float *row = plog.buf + ((size_t)st.step_index * plog.streams + s) * 3;
+        row[0] = np_[0];
+        row[1] = np_[1];
+        row[2] = np_[2];
+    }
+    st.step_index += 1;
     if (mode == MODE_PROCESS || mode == MODE_MATCH_ONLY) {
         unsigned long long it = 0;
         for (int lvl = 0; lvl < geom.levels; ++lvl) it += (lvl == 0 ? 6 : 4);
@@ -310,16 +322,13 @@ hs_match_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__
 // Every ray starts at the common begin cell; a ray is stored as its end cell (packed y<<16 | x) or
 // RAY_INVALID when updateByScan would skip it (begin == end :157, or begin/end outside :226-238).
 constexpr unsigned RAY_INVALID = 0xFFFFFFFFu;
-constexpr int TILE = 64;                 // tile edge (cells); a tile row = 64 x 8 B = 512 B
-constexpr int TILE_CELLS = TILE * TILE;  // 4096 LDS words = 16 KB
 constexpr int UPD_THREADS = 256;
-// per-cell LDS word during one tile:
-//   W_NONE            untouched
-//   W_FREE            freed by >= 1 beam, hit by none
-//   h | FF_BIT * f    hit; h = first hitting beam (< 65536); f = freed by some beam b < h first
+// two LDS words per tile cell, both updated with blind atomicMin (no read-modify-write chain):
+//   first_hit[c]  = smallest beam whose end cell is c      (NONE if none)
+//   first_free[c] = smallest beam that frees c            (NONE if none)
+// the reference's per-cell outcome depends only on these: free only -> l + lf; hit -> if freed
+// first (first_free < first_hit) ((l + lf) - lf), then + lo if l < 50.
 constexpr unsigned W_NONE = 0xFFFFFFFFu;
-constexpr unsigned W_FREE = 0xFFFFFFFEu;
-constexpr unsigned FF_BIT = 0x10000u;
 
 struct RayFrame {
     float mx, my, cs, sn;
@@ -424,184 +433,496 @@ __device__ __forceinline__ bool walk_range(const RayWalk &w, int A0, int A1, int
     return lo <= hi;
 }
 
-// ------------------------------------------------------------------- k2: tiled grid update
-// One workgroup per (stream, level).  For each 64x64 tile of the scan's bounding box:
-//   (1) end cells in the tile: LDS atomicMin of the beam index   -> first hitting beam h
-//   (2) free steps in the tile: mark W_FREE, or set FF_BIT on a hit cell when b < h
-//   (3) one coalesced read-modify-write of every touched cell (8 B) applying the reference's
-//       float sequence: free only: l + lf; hit: ((l + lf) - lf) if freed first, then + lo if < 50.
+// ------------------------------------------------------------ k2/k3: binned, tiled grid update
+// The grid update of one scan level is split into 64 x TILE_H tiles of the map:
+//   k2 hs_bin_kernel   (one workgroup per stream): builds every level's rays, walks each ray's tile
+//                      crossings in closed form (two divisions per crossing), counting-sorts the
+//                      ray segments by tile in LDS, and appends one work item per NON-EMPTY tile
+//                      (plus its segment list) to global queues.  Oversized scans fall back to one
+//                      WHOLE item per level (every ray tested against every tile of the bbox).
+//   k3 hs_tile_kernel  (grid-stride over work items): per tile, two LDS words per cell updated with
+//                      blind atomicMin --
+//                        first_hit[c]  = smallest beam whose end cell is c
+//                        first_free[c] = smallest beam that frees c
+//                      -- then ONE coalesced 8-byte read-modify-write per touched cell applying the
+//                      reference's float sequence: free only: l + lf; hit: ((l + lf) - lf) if freed
+//                      first (first_free < first_hit), then + lo if l < 50.
 // This equals running bresenhamCellFree / bresenhamCellOcc (:302-330) beam by beam.
-__global__ void __launch_bounds__(UPD_THREADS)
-hs_update_kernel(FleetGeom geom, LogOddsCell *__restrict__ cells, StreamState *__restrict__ state,
-                 const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points)
+constexpr unsigned W_NONE_ = 0xFFFFFFFFu;
+constexpr int BIN_THREADS = 256;
+constexpr int MAX_BIN_TILES = 1024;  // per level; larger bounding boxes use a WHOLE item
+constexpr int ITEM_TILE = 0, ITEM_WHOLE = 1;
+
+// Enumerate the tiles crossed by steps 0..da of a walk: f(tile_x, tile_y, lo, hi).
+template <class F>
+__device__ __forceinline__ void for_each_segment(const RayWalk &w, F f)
 {
-    extern __shared__ __attribute__((aligned(16))) unsigned smem[];
-    unsigned *tile_w = smem;                 // TILE_CELLS words
-    unsigned *rays = smem + TILE_CELLS;      // max_points packed end cells
-    __shared__ int s_bbox[4];
-    __shared__ int s_any;
-
-    // level-major block order: every stream's level 0 (the largest) is dispatched first
-    const int lvl = blockIdx.x / count;
-    const int local = blockIdx.x - lvl * count;
-    const int s = stream_begin + local;
-    const StreamState &st = state[s];
-    if (!st.do_update) return;
-    const LevelGeom &g = geom.lv[lvl];
-    const int n = st.n;
-    const int tid = threadIdx.x;
-    LogOddsCell *lc = cells + (size_t)s * geom.stream_cells + g.cell_offset;
-
-    const RayFrame fr = ray_frame(g, st);
-    const int x0 = fr.bxi, y0 = fr.byi;
-    if (tid == 0) {
-        s_bbox[0] = x0; s_bbox[1] = y0; s_bbox[2] = x0; s_bbox[3] = y0;
-        s_any = 0;
-    }
-    __syncthreads();
-    int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
-    unsigned long long L = 0, R = 0;
-    const float2 *pts = xy + (size_t)local * xy_stride;
-    for (int b = tid; b < n; b += UPD_THREADS) {
-        unsigned r = make_ray(g, fr, pts[b]);
-        rays[b] = r;
-        if (r != RAY_INVALID) {
-            int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-            bx0 = min(bx0, x1); by0 = min(by0, y1); bx1 = max(bx1, x1); by1 = max(by1, y1);
-            int adx = abs(x1 - x0), ady = abs(y1 - y0);
-            L += (unsigned long long)(max(adx, ady) + 1);
-            R += 1;
+    const int A = w.x_major ? TILE : TILE_H;   // tile extent along the major axis
+    const int Bt = w.x_major ? TILE_H : TILE;  // along the minor axis
+    int i = 0;
+    int q = 0;  // q(0) = floor(e0 / da) = 0
+    while (i <= w.da) {
+        const int a = w.a0 + w.sa * i;
+        const int b = w.b0 + w.sb * q;
+        const int ta = a / A, tb = b / Bt;
+        const int ra = w.sa > 0 ? (ta * A + A - 1 - a) : (a - ta * A);    // steps left along a
+        int iend = i + ra;
+        if (w.db > 0) {
+            const int rb = w.sb > 0 ? (tb * Bt + Bt - 1 - b) : (b - tb * Bt);  // b-steps left
+            const int qmax = q + rb;
+            const int ib = (int)(((unsigned)(qmax + 1) * (unsigned)w.da - (unsigned)w.e0 - 1u) / (unsigned)w.db);
+            if (ib < iend) iend = ib;
         }
-    }
-    if (R) {
-        atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
-        atomicMax(&s_bbox[2], bx1); atomicMax(&s_bbox[3], by1);
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        L += __shfl_xor(L, off, 64);
-        R += __shfl_xor(R, off, 64);
-    }
-    if ((tid & 63) == 0 && R) {
-        atomicAdd(&state[s].step_cells, L);
-        atomicAdd(&state[s].tot_cells, L);
-        atomicAdd(&state[s].tot_rays, R);
-    }
-    if (!__syncthreads_or(R != 0)) return;  // no ray drawn on this level
-    const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / TILE;
-    const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / TILE;
-    const int mark_free = st.mark_base + 1;  // currMarkFreeIndex (:120)
-    const int mark_occ = st.mark_base + 2;   // currMarkOccIndex  (:121)
-    const float lf = geom.lf, lo = geom.lo;
-
-    for (int ty = ty0; ty <= ty1; ++ty) {
-        for (int tx = tx0; tx <= tx1; ++tx) {
-            const int X0 = tx * TILE, Y0 = ty * TILE;
-            const int X1 = X0 + TILE, Y1 = Y0 + TILE;
-            // clear the tile words
-            for (int k = tid; k < TILE_CELLS / 4; k += UPD_THREADS)
-                reinterpret_cast<uint4 *>(tile_w)[k] = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
-            __syncthreads();
-            // (1) hits
-            bool any = false;
-            for (int b = tid; b < n; b += UPD_THREADS) {
-                unsigned r = rays[b];
-                if (r == RAY_INVALID) continue;
-                int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-                if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {
-                    atomicMin(&tile_w[(y1 - Y0) * TILE + (x1 - X0)], (unsigned)b);
-                    any = true;
-                }
-            }
-            __syncthreads();
-            // (2) free steps
-            for (int b = tid; b < n; b += UPD_THREADS) {
-                unsigned r = rays[b];
-                if (r == RAY_INVALID) continue;
-                int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-                if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
-                RayWalk w = ray_walk(x0, y0, x1, y1);
-                int lo_i, hi_i;
-                bool hit = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i) : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
-                if (!hit) continue;
-                if (hi_i > w.da - 1) hi_i = w.da - 1;  // free steps only
-                if (lo_i > hi_i) continue;
-                any = true;
-                const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
-                int q = (int)(num / (unsigned)w.da);
-                int err = (int)(num - (unsigned)q * (unsigned)w.da);
-                int a = w.a0 + w.sa * lo_i;
-                int bb = w.b0 + w.sb * q;
-                for (int i = lo_i; i <= hi_i; ++i) {
-                    int cx = w.x_major ? a : bb;
-                    int cy = w.x_major ? bb : a;
-                    unsigned *wp = &tile_w[(cy - Y0) * TILE + (cx - X0)];
-                    unsigned v = *wp;
-                    if (v >= W_FREE) {
-                        *wp = W_FREE;
-                    } else if ((unsigned)b < (v & 0xFFFFu)) {
-                        *wp = v | FF_BIT;  // freed by an earlier beam than the first hit
-                    }
-                    a += w.sa;
-                    err += w.db;
-                    if (err >= w.da) {
-                        err -= w.da;
-                        bb += w.sb;
-                    }
-                }
-            }
-            if (any) s_any = 1;
-            __syncthreads();
-            if (s_any) {
-                // (3) apply: wave w handles rows w, w+4, ...; lane = column -> 512 B coalesced rows
-                const int col = tid & 63;
-                const int gx = X0 + col;
-                for (int row = tid >> 6; row < TILE; row += UPD_THREADS / 64) {
-                    const int gy = Y0 + row;
-                    unsigned v = tile_w[row * TILE + col];
-                    if (v == W_NONE || gx >= g.sx || gy >= g.sy) continue;
-                    LogOddsCell *cp = lc + (size_t)gy * g.sx + gx;
-                    LogOddsCell c = *cp;
-                    if (v == W_FREE) {
-                        c.l = c.l + lf;        // updateSetFree (GridMapLogOdds.h:120-124)
-                        c.upd = mark_free;
-                    } else {
-                        if (v & FF_BIT) {
-                            c.l = c.l + lf;    // bresenhamCellFree by an earlier beam
-                            c.l = c.l - lf;    // updateUnsetFree (GridMapLogOdds.h:126-129)
-                        }
-                        if (c.l < 50.0f) c.l = c.l + lo;  // updateSetOccupied (:108-114)
-                        c.upd = mark_occ;
-                    }
-                    *cp = c;
-                }
-            }
-            __syncthreads();
-            if (tid == 0) s_any = 0;
-        }
+        if (iend > w.da) iend = w.da;
+        if (w.x_major) f(ta, tb, i, iend);
+        else f(tb, ta, i, iend);
+        i = iend + 1;
+        q = (int)(((unsigned)w.e0 + (unsigned)i * (unsigned)w.db) / (unsigned)w.da);
     }
 }
 
+// block-wide exclusive scan of v (256 threads); returns the exclusive prefix, *total = sum
+__device__ __forceinline__ int block_exscan(int v, int *s_wave, int *total)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int t = __shfl_up(x, off, 64);
+        if (lane >= off) x += t;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < BIN_THREADS / 64; ++k) {
+        const int ws = s_wave[k];
+        if (k < wave) base += ws;
+        tot += ws;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+__global__ void __launch_bounds__(BIN_THREADS)
+hs_bin_kernel(FleetGeom geom, StreamState *__restrict__ state, const float2 *__restrict__ xy, int xy_stride,
+              int stream_begin, int max_points, unsigned *__restrict__ rays_g, uint4 *__restrict__ segs,
+              WorkItem *__restrict__ items, WorkItem *__restrict__ wholes, WorkQueue *__restrict__ wq,
+              unsigned seg_cap, unsigned item_cap)
+{
+    __shared__ int s_bbox[4];
+    __shared__ int s_cnt[MAX_BIN_TILES];
+    __shared__ int s_off[MAX_BIN_TILES];
+    __shared__ unsigned s_rows[MAX_BIN_TILES];  // per tile: mask of tile rows touched
+    __shared__ int s_wave[BIN_THREADS / 64];
+    __shared__ unsigned s_base[2];
+    const int local = blockIdx.x;
+    const int s = stream_begin + local;
+    const StreamState &st = state[s];
+    if (!st.do_update) return;
+    const int n = st.n;
+    const int tid = threadIdx.x;
+    const float2 *pts = xy + (size_t)local * xy_stride;
+    unsigned long long Ltot = 0, Rtot = 0;
+
+    for (int lvl = 0; lvl < geom.levels; ++lvl) {
+        const LevelGeom &g = geom.lv[lvl];
+        unsigned *rays = rays_g + ((size_t)s * geom.levels + lvl) * max_points;
+        const RayFrame fr = ray_frame(g, st);
+        const int x0 = fr.bxi, y0 = fr.byi;
+        if (tid == 0) {
+            s_bbox[0] = x0; s_bbox[1] = y0; s_bbox[2] = x0; s_bbox[3] = y0;
+        }
+        __syncthreads();
+        int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0, R = 0;
+        for (int b = tid; b < n; b += BIN_THREADS) {
+            unsigned r = make_ray(g, fr, pts[b]);
+            rays[b] = r;
+            if (r != RAY_INVALID) {
+                int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+                bx0 = min(bx0, x1); by0 = min(by0, y1); bx1 = max(bx1, x1); by1 = max(by1, y1);
+                Ltot += (unsigned long long)(max(abs(x1 - x0), abs(y1 - y0)) + 1);
+                R += 1;
+            }
+        }
+        Rtot += R;
+        if (R) {
+            atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
+            atomicMax(&s_bbox[2], bx1); atomicMax(&s_bbox[3], by1);
+        }
+        if (!__syncthreads_or(R != 0)) continue;  // nothing drawn on this level
+        const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / TILE_H;
+        const int ntx = s_bbox[2] / TILE - tx0 + 1, nty = s_bbox[3] / TILE_H - ty0 + 1;
+        const int nt = ntx * nty;
+        const unsigned begin_xy = (unsigned)x0 | ((unsigned)y0 << 16);
+        bool whole = nt > MAX_BIN_TILES;
+        if (!whole) {
+            for (int t = tid; t < nt; t += BIN_THREADS) {
+                s_cnt[t] = 0;
+                s_rows[t] = 0;
+            }
+            __syncthreads();
+            // pass 1: count segments per tile
+            for (int b = tid; b < n; b += BIN_THREADS) {
+                unsigned r = rays[b];
+                if (r == RAY_INVALID) continue;
+                RayWalk w = ray_walk(x0, y0, (int)(r & 0xFFFFu), (int)(r >> 16));
+                for_each_segment(w, [&](int tx, int ty, int lo, int hi) {
+                    const int t = (ty - ty0) * ntx + (tx - tx0);
+                    atomicAdd(&s_cnt[t], 1);
+                    // rows spanned by steps lo..hi (monotone along the walk)
+                    int ylo, yhi;
+                    if (w.x_major) {
+                        ylo = w.b0 + w.sb * (int)(((unsigned)w.e0 + (unsigned)lo * (unsigned)w.db) / (unsigned)w.da);
+                        yhi = w.b0 + w.sb * (int)(((unsigned)w.e0 + (unsigned)hi * (unsigned)w.db) / (unsigned)w.da);
+                    } else {
+                        ylo = w.a0 + w.sa * lo;
+                        yhi = w.a0 + w.sa * hi;
+                    }
+                    const int r0 = min(ylo, yhi) - ty * TILE_H, r1 = max(ylo, yhi) - ty * TILE_H;
+                    const unsigned m1 = r1 >= 31 ? 0xFFFFFFFFu : ((2u << r1) - 1u);
+                    const unsigned m0 = (1u << r0) - 1u;
+                    atomicOr(&s_rows[t], m1 & ~m0);
+                });
+            }
+            __syncthreads();
+            // exclusive scans: segment offsets and non-empty tile ranks (each thread owns a chunk)
+            const int per = (nt + BIN_THREADS - 1) / BIN_THREADS;
+            const int t0 = tid * per, t1 = min(nt, t0 + per);
+            int csum = 0, cne = 0;
+            for (int t = t0; t < t1; ++t) {
+                csum += s_cnt[t];
+                cne += s_cnt[t] > 0;
+            }
+            int seg_total, ne_total;
+            int seg_pre = block_exscan(csum, s_wave, &seg_total);
+            int ne_pre = block_exscan(cne, s_wave, &ne_total);
+            if (tid == 0) {
+                unsigned sb = atomicAdd(&wq->seg_used, (unsigned)seg_total);
+                unsigned ib = atomicAdd(&wq->item_used, (unsigned)ne_total);
+                if (sb + (unsigned)seg_total > seg_cap || ib + (unsigned)ne_total > item_cap) {
+                    atomicAdd(&wq->overflow, 1u);
+                    sb = 0xFFFFFFFFu;  // -> WHOLE item (the reserved ranges stay unused)
+                }
+                s_base[0] = sb;
+                s_base[1] = ib;
+            }
+            __syncthreads();
+            const unsigned seg_base = s_base[0], item_base = s_base[1];
+            whole = seg_base == 0xFFFFFFFFu;
+            if (!whole) {
+                // offsets + work items for this thread's chunk of tiles; s_off becomes the fill cursor
+                for (int t = t0; t < t1; ++t) {
+                    const int c = s_cnt[t];
+                    s_off[t] = seg_pre;
+                    if (c > 0) {
+                        WorkItem it;
+                        it.s = s;
+                        it.lvl_kind = lvl | (ITEM_TILE << 8);
+                        it.tile_xy = (unsigned)(tx0 + t % ntx) | ((unsigned)(ty0 + t / ntx) << 16);
+                        it.begin_xy = begin_xy;
+                        it.seg_begin = seg_base + (unsigned)seg_pre;
+                        it.seg_count = (unsigned)c;
+                        it.mark_base = (unsigned)st.mark_base;
+                        it.n = s_rows[t];  // tile items: touched-row mask
+                        items[item_base + (unsigned)ne_pre] = it;
+                        ++ne_pre;
+                    }
+                    seg_pre += c;
+                }
+                __syncthreads();
+                // pass 2: scatter segments {beam | lo<<16, hi}
+                for (int b = tid; b < n; b += BIN_THREADS) {
+                    unsigned r = rays[b];
+                    if (r == RAY_INVALID) continue;
+                    RayWalk w = ray_walk(x0, y0, (int)(r & 0xFFFFu), (int)(r >> 16));
+                    for_each_segment(w, [&](int tx, int ty, int lo, int hi) {
+                        const int slot = atomicAdd(&s_off[(ty - ty0) * ntx + (tx - tx0)], 1);
+                        segs[seg_base + (unsigned)slot] = make_uint4((unsigned)b | ((unsigned)lo << 16), (unsigned)hi, r, 0u);
+                    });
+                }
+            }
+        }
+        if (whole && tid == 0) {
+            const unsigned k = atomicAdd(&wq->whole_used, 1u);
+            WorkItem it;
+            it.s = s;
+            it.lvl_kind = lvl | (ITEM_WHOLE << 8);
+            it.tile_xy = (unsigned)tx0 | ((unsigned)ty0 << 16);
+            it.begin_xy = begin_xy;
+            it.seg_begin = (unsigned)ntx | ((unsigned)nty << 16);
+            it.seg_count = 0;
+            it.mark_base = (unsigned)st.mark_base;
+            it.n = (unsigned)n;
+            wholes[k] = it;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        Ltot += __shfl_xor(Ltot, off, 64);
+        Rtot += __shfl_xor(Rtot, off, 64);
+    }
+    if ((tid & 63) == 0 && Rtot) {
+        atomicAdd(&state[s].step_cells, Ltot);
+        atomicAdd(&state[s].tot_cells, Ltot);
+        atomicAdd(&state[s].tot_rays, Rtot);
+    }
+}
+
+#ifndef S2D_TILE_MINW
+#define S2D_TILE_MINW 1
+#endif
+// Diagnostic build only (-DS2D_STAMPS): per-phase s_memtime sums of hs_tile_kernel, wave 0 of each
+// workgroup: [0] wait+clear, [1] raster, [2] apply, [3] tiles, [4] workgroup lifetime.
+__device__ unsigned long long g_stamps[8];
+#ifdef S2D_STAMPS
+#define S2D_STAMP(v) do { __builtin_amdgcn_sched_barrier(0); v = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define S2D_STAMP(v) do { } while (0)
+#endif
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt) but not
+// for its global loads/stores (__syncthreads' release fence would also drain vmcnt, serialising the
+// prefetched cell loads and the previous tile's stores into every barrier).
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Tile kernel: ONE WAVE per workgroup and per tile, so there is no workgroup barrier and many tiles
+// are in flight per CU (latency, not issue, bounds this phase).  Workgroup w takes items w, w+G, ...
+// (G = grid); the next item and its first 64 segments are loaded one tile ahead.
+//   LDS: two key arrays per tile, rows padded to 65 words (vertical neighbours on different banks);
+//        key = (0xFFFF - gen) << 16 | beam, gen = 1 + tiles processed by this wave, so atomicMin
+//        overwrites stale keys of earlier tiles and no per-tile clear is needed.
+//   raster: one segment per lane (closed-form start, Bresenham increments), blind LDS atomicMin.
+//        (Flattening the (segment, step) pairs over the lanes was measured 1.9x slower: its serial
+//        LDS reads are not hidden at this occupancy.)
+//   apply: only the tile rows flagged in the item's row mask are loaded (issued at tile start,
+//        overlapping the raster); touched cells are stored; nothing waits for the stores.
+constexpr int TILE_THREADS = 64;
+constexpr int LDS_STRIDE = TILE + 1;
+constexpr int TILE_WORDS = TILE_H * LDS_STRIDE;
+static_assert(TILE_H <= 32, "row masks are 32-bit");
+
+__global__ void __launch_bounds__(TILE_THREADS, S2D_TILE_MINW)
+hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__restrict__ state,
+               const unsigned *__restrict__ rays_g, const uint4 *__restrict__ segs, const WorkItem *__restrict__ items,
+               const WorkItem *__restrict__ wholes, const WorkQueue *__restrict__ wq, int max_points)
+{
+    __shared__ __attribute__((aligned(16))) unsigned s_hit[TILE_WORDS];
+    __shared__ __attribute__((aligned(16))) unsigned s_free[TILE_WORDS];
+    const unsigned n_items = wq->item_used < wq->item_cap ? wq->item_used : wq->item_cap;
+    const unsigned n_total = n_items + wq->whole_used;
+    const int lane = threadIdx.x;
+    const float lf = geom.lf, lo = geom.lo;
+    unsigned long long ts0 = 0, ta = 0, tb = 0, tc = 0, td = 0, acc0 = 0, acc1 = 0, acc2 = 0, ntiles = 0;
+    S2D_STAMP(ts0);
+    for (int k = lane; k < TILE_WORDS; k += TILE_THREADS) {
+        s_hit[k] = 0xFFFFFFFFu;
+        s_free[k] = 0xFFFFFFFFu;
+    }
+    unsigned gen = 1;  // gen 0's key prefix 0xFFFF would alias the 0xFFFFFFFF fill
+    unsigned it = blockIdx.x;
+    WorkItem nxt;
+    uint4 sg_nxt = make_uint4(0, 0, RAY_INVALID, 0);
+    if (it < n_total) {
+        nxt = it < n_items ? items[it] : wholes[it - n_items];
+        if ((nxt.lvl_kind >> 8) == ITEM_TILE && (unsigned)lane < nxt.seg_count) sg_nxt = segs[nxt.seg_begin + lane];
+    }
+    for (; it < n_total; it += gridDim.x) {
+        S2D_STAMP(ta);
+        const WorkItem item = nxt;
+        const uint4 sg_cur = sg_nxt;
+        const unsigned itn = it + gridDim.x;
+        if (itn < n_total) nxt = itn < n_items ? items[itn] : wholes[itn - n_items];  // prefetch item
+        const int s = item.s;
+        const int lvl = item.lvl_kind & 0xFF;
+        const int kind = item.lvl_kind >> 8;
+        const LevelGeom &g = geom.lv[lvl];
+        const int mark_free = (int)item.mark_base + 1;  // currMarkFreeIndex (:120)
+        const int mark_occ = (int)item.mark_base + 2;   // currMarkOccIndex  (:121)
+        float *lvw = cells + (size_t)s * geom.stream_words + g.word_offset;
+        const int x0 = (int)(item.begin_xy & 0xFFFFu), y0 = (int)(item.begin_xy >> 16);
+        const int ttx0 = (int)(item.tile_xy & 0xFFFFu), tty0 = (int)(item.tile_xy >> 16);
+        const int ntx = kind == ITEM_TILE ? 1 : (int)(item.seg_begin & 0xFFFFu);
+        const int nty = kind == ITEM_TILE ? 1 : (int)(item.seg_begin >> 16);
+        const unsigned rowmask = kind == ITEM_TILE ? item.n : 0xFFFFFFFFu;
+        for (int tt = 0; tt < ntx * nty; ++tt) {
+            if (gen == 0xFFFFu) {  // key space exhausted: reset (never reached at realistic sizes)
+                for (int k = lane; k < TILE_WORDS; k += TILE_THREADS) {
+                    s_hit[k] = 0xFFFFFFFFu;
+                    s_free[k] = 0xFFFFFFFFu;
+                }
+                gen = 1;
+            }
+            const unsigned gkey = (0xFFFFu - gen) << 16;
+            const int X0 = (ttx0 + tt % ntx) * TILE, Y0 = (tty0 + tt / ntx) * TILE_H;
+            const int gx = X0 + lane;
+            const bool colok = gx < g.sx;
+            // this tile's contiguous 16 KB block: log-odds plane then updateIndex plane
+            float *tl = lvw + (size_t)((ttx0 + tt % ntx) + (tty0 + tt / ntx) * g.tiles_x) * TILE_BLOCK_WORDS;
+            int *tu = reinterpret_cast<int *>(tl + TILE_CELLS);
+            float cl[TILE_H];
+#pragma unroll
+            for (int row = 0; row < TILE_H; ++row) {
+                const int gy = Y0 + row;
+#ifdef S2D_ABL_NOLOAD
+                cl[row] = (float)row;
+#else
+                if (((rowmask >> row) & 1u) && colok && gy < g.sy) cl[row] = tl[row * TILE + lane];
+#endif
+            }
+            S2D_STAMP(tb);
+            bool any = false;
+            if (kind == ITEM_TILE) {
+                any = item.seg_count > 0;
+                uint4 sg = sg_cur;
+                for (unsigned k = lane; k < item.seg_count; k += TILE_THREADS) {
+                    if (k != (unsigned)lane) sg = segs[item.seg_begin + k];
+                    const unsigned key = gkey | (sg.x & 0xFFFFu);
+                    RayWalk w = ray_walk(x0, y0, (int)(sg.z & 0xFFFFu), (int)(sg.z >> 16));
+                    const int slo = (int)(sg.x >> 16), shi = (int)sg.y;
+                    const unsigned num = (unsigned)w.e0 + (unsigned)slo * (unsigned)w.db;
+                    const int qq = (int)(num / (unsigned)w.da);
+                    int err = (int)(num - (unsigned)qq * (unsigned)w.da);
+                    const int la = w.x_major ? 1 : LDS_STRIDE;
+                    const int lb = w.x_major ? LDS_STRIDE : 1;
+                    int li = (w.a0 + w.sa * slo - (w.x_major ? X0 : Y0)) * la + (w.b0 + w.sb * qq - (w.x_major ? Y0 : X0)) * lb;
+                    const int da_step = w.sa * la, db_step = w.sb * lb;
+                    const int ifree = min(shi, w.da - 1);
+                    for (int i = slo; i <= ifree; ++i) {
+                        atomicMin(&s_free[li], key);  // bresenhamCellFree (:302-312)
+                        li += da_step;
+                        err += w.db;
+                        if (err >= w.da) {
+                            err -= w.da;
+                            li += db_step;
+                        }
+                    }
+                    if (shi == w.da) atomicMin(&s_hit[li], key);  // end cell (:265-266)
+                }
+            } else {
+                // fallback for oversized scans: every ray against this tile (closed-form step range)
+                const unsigned *rays = rays_g + ((size_t)s * geom.levels + lvl) * max_points;
+                const int n = (int)item.n;
+                const int X1 = X0 + TILE, Y1 = Y0 + TILE_H;
+                for (int b = lane; b < n; b += TILE_THREADS) {
+                    const unsigned r = rays[b];
+                    if (r == RAY_INVALID) continue;
+                    const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+                    if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
+                    RayWalk w = ray_walk(x0, y0, x1, y1);
+                    int lo_i, hi_i;
+                    bool in = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i)
+                                        : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
+                    if (!in) continue;
+                    any = true;
+                    const unsigned key = gkey | (unsigned)b;
+                    const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
+                    const int qq = (int)(num / (unsigned)w.da);
+                    int err = (int)(num - (unsigned)qq * (unsigned)w.da);
+                    const int la = w.x_major ? 1 : LDS_STRIDE;
+                    const int lb = w.x_major ? LDS_STRIDE : 1;
+                    int li = (w.a0 + w.sa * lo_i - (w.x_major ? X0 : Y0)) * la + (w.b0 + w.sb * qq - (w.x_major ? Y0 : X0)) * lb;
+                    const int ifree = min(hi_i, w.da - 1);
+                    for (int i = lo_i; i <= ifree; ++i) {
+                        atomicMin(&s_free[li], key);
+                        li += w.sa * la;
+                        err += w.db;
+                        if (err >= w.da) {
+                            err -= w.da;
+                            li += w.sb * lb;
+                        }
+                    }
+                    if (hi_i == w.da) atomicMin(&s_hit[li], key);
+                }
+            }
+            // prefetch the next item's first segments (the item load was issued at the top)
+            if (tt == ntx * nty - 1 && itn < n_total && (nxt.lvl_kind >> 8) == ITEM_TILE &&
+                (unsigned)lane < nxt.seg_count)
+                sg_nxt = segs[nxt.seg_begin + lane];
+            S2D_STAMP(tc);
+            if (__any(any)) {
+                // apply: lane = column -> 256 B / 512 B coalesced row accesses
+#pragma unroll
+                for (int row = 0; row < TILE_H; ++row) {
+                    const int gy = Y0 + row;
+                    if (!((rowmask >> row) & 1u) || !colok || gy >= g.sy) continue;
+                    const unsigned hk = s_hit[row * LDS_STRIDE + lane];
+                    const unsigned fk = s_free[row * LDS_STRIDE + lane];
+                    const bool hit = (hk & 0xFFFF0000u) == gkey;
+                    const bool fre = (fk & 0xFFFF0000u) == gkey;
+                    if (!hit && !fre) continue;
+                    float l = cl[row];
+                    int upd;
+                    if (!hit) {
+                        l = l + lf;        // updateSetFree (GridMapLogOdds.h:120-124)
+                        upd = mark_free;
+                    } else {
+                        if (fre && (fk & 0xFFFFu) < (hk & 0xFFFFu)) {
+                            l = l + lf;    // bresenhamCellFree by an earlier beam
+                            l = l - lf;    // updateUnsetFree (GridMapLogOdds.h:126-129)
+                        }
+                        if (l < 50.0f) l = l + lo;  // updateSetOccupied (:108-114)
+                        upd = mark_occ;
+                    }
+#ifdef S2D_ABL_NOSTORE
+                    asm volatile("" ::"v"(l), "v"(upd));
+#else
+                    tl[row * TILE + lane] = l;
+                    tu[row * TILE + lane] = upd;
+#endif
+                }
+            }
+            ++gen;
+            S2D_STAMP(td);
+            acc0 += tb - ta;
+            acc1 += tc - tb;
+            acc2 += td - tc;
+            ntiles += 1;
+            ta = td;
+        }
+    }
+#ifdef S2D_STAMPS
+    unsigned long long te;
+    S2D_STAMP(te);
+    if (lane == 0) {
+        atomicAdd(&g_stamps[0], acc0);
+        atomicAdd(&g_stamps[1], acc1);
+        atomicAdd(&g_stamps[2], acc2);
+        atomicAdd(&g_stamps[3], ntiles);
+        atomicAdd(&g_stamps[4], te - ts0);
+    }
+#else
+    (void)ts0; (void)acc0; (void)acc1; (void)acc2; (void)ntiles; (void)tb; (void)tc; (void)td;
+#endif
+}
 
 // --------------------------------------------------------------------------- utility kernels
-__global__ void hs_fill_cells_kernel(LogOddsCell *__restrict__ cells, size_t n)
+__global__ void hs_fill_cells_kernel(float *__restrict__ words, size_t n)
 {
-    // LogOddsCell::resetGridCell  H/map/GridMapLogOdds.h:76-80
+    // LogOddsCell::resetGridCell  H/map/GridMapLogOdds.h:76-80 : log-odds plane 0.0f, updateIndex plane -1
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     size_t stride = (size_t)gridDim.x * blockDim.x;
     for (; i < n; i += stride) {
-        cells[i].l = 0.0f;
-        cells[i].upd = -1;
+        if ((i / TILE_CELLS) & 1) reinterpret_cast<int *>(words)[i] = -1;
+        else words[i] = 0.0f;
     }
 }
 
 // HectorMappingRos::publishMap cell conversion  lesson4/src/hector_mapping/hector_slam.cc:287-304
-__global__ void hs_publish_kernel(const LogOddsCell *__restrict__ cells, int8_t *__restrict__ out, size_t n)
+// (tiled storage -> row-major int8)
+__global__ void hs_publish_kernel(const float *__restrict__ lvw, LevelGeom g, int8_t *__restrict__ out)
 {
+    const size_t n = (size_t)g.sx * g.sy;
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     size_t stride = (size_t)gridDim.x * blockDim.x;
     for (; i < n; i += stride) {
-        float l = cells[i].l;
+        const int x = (int)(i % g.sx), y = (int)(i / g.sx);
+        const float l = lvw[cell_word(g, x, y)];
         out[i] = l < 0.0f ? (int8_t)0 : (l > 0.0f ? (int8_t)100 : (int8_t)-1);
     }
 }

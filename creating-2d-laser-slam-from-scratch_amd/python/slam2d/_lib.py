@@ -13,7 +13,7 @@ import subprocess
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CSRC = os.path.join(PKG_ROOT, "csrc")
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libslam2d.so")
+LIB_PATH = os.environ.get("SLAM2D_LIB") or os.path.join(PKG_ROOT, "lib", "libslam2d.so")
 
 _f, _i, _p = C.c_float, C.c_int, C.c_void_p
 _LIB = None
@@ -52,7 +52,9 @@ def _declare(L):
     L.hs_step_batch_device.argtypes = [_p, _i, _i, _p, _i, _p, _p, _p, _p]
     L.hs_get_poses.argtypes = [_p, _p, _p, _p, _p]
     L.hs_get_counters.argtypes = [_p, _p, _i]
+    L.hs_get_queue_stats.argtypes = [_p, _p, _i]
     L.hs_get_device_buffers.argtypes = [_p, P(_p), P(C.c_size_t), P(C.c_size_t)]
+    L.hs_set_pose_log.argtypes = [_p, _p, _i, _i]
     L.hs_get_stream.restype = _p
     L.hs_get_stream.argtypes = [_p]
     L.hs_set_timing.argtypes = [_p, _i]

@@ -203,6 +203,16 @@ class HectorFleet:
         check(self.L.hs_get_counters(self.h, _fp(o), 1 if reset else 0), "hs_get_counters")
         return {"cells": int(o[0]), "rays": int(o[1]), "gn_points": int(o[2]), "updates": int(o[3]), "steps": int(o[4])}
 
+    def set_pose_log(self, d_buf: int, streams: int, capacity: int):
+        """Device pose log (float32 [capacity][streams][3]) filled by every step; d_buf = 0 disables."""
+        check(self.L.hs_set_pose_log(self.h, C.c_void_p(d_buf or None), int(streams), int(capacity)), "hs_set_pose_log")
+
+    def queue_stats(self, reset_stamps=True):
+        o = np.zeros(8, np.int64)
+        check(self.L.hs_get_queue_stats(self.h, _fp(o), 1 if reset_stamps else 0), "hs_get_queue_stats")
+        return {"items": int(o[0]), "segments": int(o[1]), "whole": int(o[2]), "overflow": int(o[3]),
+                "cyc_setup": int(o[4]), "cyc_raster": int(o[5]), "cyc_apply": int(o[6]), "tiles": int(o[7])}
+
     def stream_handle(self) -> int:
         return int(self.L.hs_get_stream(self.h) or 0)
 
@@ -210,10 +220,10 @@ class HectorFleet:
         check(self.L.hs_set_timing(self.h, 1 if enable else 0), "hs_set_timing")
 
     def kernel_times(self, reset=True):
-        ms = np.zeros(2, np.float64)
-        n = np.zeros(2, np.int64)
+        ms = np.zeros(3, np.float64)
+        n = np.zeros(3, np.int64)
         check(self.L.hs_get_kernel_times(self.h, _fp(ms), _fp(n), 1 if reset else 0), "hs_get_kernel_times")
-        names = ("match", "update")
+        names = ("match", "bin", "tile")
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}
 
 

@@ -105,17 +105,27 @@ int hs_get_poses(hs_ctx *ctx, float *poses_out, float *covs_out, int *did_update
  * out[0] Σ cells traversed (Σ abs_da+1), out[1] valid rays, out[2] Σ points x GN iterations,
  * out[3] map updates, out[4] steps.  reset != 0 zeroes them afterwards. */
 int hs_get_counters(hs_ctx *ctx, int64_t out[5], int reset);
-/* Device pointer of the per-stream state array and of the cell storage (for zero-copy consumers). */
-int hs_get_device_buffers(hs_ctx *ctx, void **cells, size_t *cells_bytes, size_t *stream_cells);
+/* Grid-update queue of the last step: out[0] tile work items, out[1] ray segments, out[2] WHOLE
+ * (unbinned) level items, out[3] overflow events (cumulative); out[4..7] diagnostic-build phase
+ * cycle sums of hs_tile_kernel (setup+clear, raster, apply, tiles; zero in normal builds). */
+int hs_get_queue_stats(hs_ctx *ctx, int64_t out[8], int reset_stamps);
+/* Device cell storage (for zero-copy consumers): per stream `stream_words` 4-byte words; each level
+ * is a grid of 64 x 32-cell tiles, each tile 16 KB = 2048 log-odds floats (row-major) followed by
+ * 2048 int32 updateIndex values (DESIGN.md "Data layout in HBM"). */
+int hs_get_device_buffers(hs_ctx *ctx, void **cells, size_t *cells_bytes, size_t *stream_words);
+/* Optional device pose log: every step appends the scan-match pose (float3) of streams [0, streams)
+ * at row = steps since hs_reset, i.e. d_buf[(row*streams + s)*3]; rows >= capacity are dropped.
+ * d_buf NULL disables.  The caller owns d_buf (device memory of >= capacity*streams*3 floats). */
+int hs_set_pose_log(hs_ctx *ctx, float *d_buf, int streams, int capacity);
 /* The context's own HIP stream (hipStream_t as void*). */
 void *hs_get_stream(hs_ctx *ctx);
 
 /* ---- measurement ----------------------------------------------------------------------------- */
 /* Kernel timing with HIP events recorded on the launch stream around every kernel of every step
- * (enable = 1).  hs_get_kernel_times fills, for the 2 kernels {hs_match_kernel, hs_update_kernel},
- * the accumulated milliseconds and launch counts since the last reset (synchronises). */
+ * (enable = 1).  hs_get_kernel_times fills, for the 3 kernels {hs_match_kernel, hs_bin_kernel,
+ * hs_tile_kernel}, the accumulated milliseconds and launch counts since the last reset (synchronises). */
 int hs_set_timing(hs_ctx *ctx, int enable);
-int hs_get_kernel_times(hs_ctx *ctx, double ms_out[2], int64_t launches_out[2], int reset);
+int hs_get_kernel_times(hs_ctx *ctx, double ms_out[3], int64_t launches_out[3], int reset);
 
 #ifdef __cplusplus
 }

@@ -77,6 +77,21 @@ def test_out_of_map_beams_small_map(gpu, scans):
     _run_pair(1, 256, scans, n_scans=15, thresholds=(-1.0, -1.0))
 
 
+@pytest.mark.parametrize("cap_env", ["SLAM2D_SEG_CAP", "SLAM2D_ITEM_CAP"])
+def test_unbinned_fallback_bitexact(gpu, scans, monkeypatch, cap_env):
+    """Queue overflow -> WHOLE items (every ray tested against every tile of the level's bbox)."""
+    monkeypatch.setenv(cap_env, "8")
+    fleet, _ = _run_pair(2, 1024, scans, n_scans=8, thresholds=(-1.0, -1.0), stream=2)
+    q = fleet.queue_stats()
+    assert q["whole"] > 0 and q["overflow"] > 0, q
+
+
+def test_binned_path_used(gpu, scans):
+    fleet, _ = _run_pair(3, 1024, scans, n_scans=3, thresholds=(-1.0, -1.0))
+    q = fleet.queue_stats()
+    assert q["whole"] == 0 and q["overflow"] == 0 and q["items"] > 0, q
+
+
 def test_pose_tolerance_vs_reference_order(gpu, scans):
     """GPU trajectory vs the oracle in the reference's sequential summation order."""
     n = 30

@@ -39,7 +39,8 @@ CONFIGS = {
     # BASELINE configs[2]: 3-level 4096^2
     "c3": dict(map_size=4096, levels=3, streams=256),
 }
-KERNELS = ("match", "bin", "tile")
+KERNELS = ("match", "bin", "update")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")  # written by tools/summarize_profile.py
 
 
 def log(*a):
@@ -54,31 +55,87 @@ def algorithmic_bytes(ctr: dict, levels: int) -> dict:
     b_update = ctr["cells"] * 16
     # hs_bin_kernel: reads every level's points (8 B) and writes the packed end cell (4 B) per ray
     b_bin = ctr["rays"] * 12
-    return {"match": b_match, "bin": b_bin, "tile": b_update, "total": b_match + b_update,
+    return {"match": b_match, "bin": b_bin, "update": b_update, "total": b_match + b_update,
             "read_only": b_match + ctr["cells"] * 8}
 
 
-def cpu_baseline(cfg, seconds=10.0, max_scans=4000):
-    """Time the CPU oracle (C restatement at -O2, reference sequential order, 1 core) on a bounded
-    sample of the same workload: one stream, consecutive scans, forced map update each scan."""
+def kernel_symbol(dom: str, ktimes: dict) -> str:
+    if dom == "update":
+        return "hs_tile_kernel" if ktimes["bin"][1] > 0 else "hs_update_kernel"
+    return f"hs_{dom}_kernel"
+
+
+def pmc_traffic(kernel: str, cfg_name: str, streams: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this exact
+    workload (tools/profile_gpu.sh + tools/summarize_profile.py): FETCH_SIZE x 2 (gfx950 tallies
+    128-B read requests at 64 B, MI355X_MICROARCH.md) + WRITE_SIZE, both KB -> bytes."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for e in d.get("entries", []):
+        if e.get("kernel") == kernel and e.get("config") == cfg_name and e.get("streams") == streams:
+            return e
+    return None
+
+
+def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
+    """Attainable device-to-device copy bandwidth (read + write bytes / time), torch copy_."""
+    import torch
+
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        b.copy_(a)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del a, b
+    torch.cuda.empty_cache()
+    return 2.0 * nbytes * reps / dt / 1e9
+
+
+def cpu_baseline(cfg, seconds=10.0, seconds_o0=4.0):
+    """Time the CPU oracle (C restatement at -O3, reference sequential order, 1 core, exactly one
+    stream as the reference node runs) on a bounded sample of the same workload: one stream,
+    consecutive scans, forced map update each scan.  The -O0 build (the reference ships Debug,
+    lesson4/CMakeLists.txt:6) is timed beside it on the same scans."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from slam2d import synth
 
     n_scans = 600
     S = synth.make_streams(1, n_scans, seed=999)
-    h = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0)
-    h.set_update_factors(0.4, 0.9)
-    h.set_thresholds(-1.0, -1.0)
-    done = 0
-    t0 = time.perf_counter()
-    while done < n_scans and time.perf_counter() - t0 < seconds:
-        h.process(S.points[0, done, : S.counts[0, done]])
-        done += 1
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "scans/s", "cores": 1, "kind": "port",
+
+    def run(variant, budget):
+        h = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0, lib_variant=variant)
+        h.set_update_factors(0.4, 0.9)
+        h.set_thresholds(-1.0, -1.0)
+        done = 0
+        t0 = time.perf_counter()
+        while done < n_scans and time.perf_counter() - t0 < budget:
+            h.process(S.points[0, done, : S.counts[0, done]])
+            done += 1
+        dt = time.perf_counter() - t0
+        h.close()
+        return done, done / dt
+
+    done, v = run("", seconds)
+    done0, v0 = run("O0", seconds_o0)
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"value": v, "unit": "scans/s", "cores": 1, "kind": "port",
             "sample": f"1 stream x {done} consecutive synthetic 1081-beam scans, {cfg['map_size']}^2 x "
-                      f"{cfg['levels']} levels, forced map update, oracle/hector_oracle.c -O2 single thread"}
+                      f"{cfg['levels']} levels, forced map update, oracle/hector_oracle.c -O3 single thread",
+            "value_O0": v0, "sample_O0": f"same stream, first {done0} scans, -O0 build", "cpu_model": cpu_model}
 
 
 def pose_check(cfg, S, gpu_poses):
@@ -119,6 +176,7 @@ def main():
     ap.add_argument("--config", default="northstar", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--no-copy-probe", action="store_true", help="skip the copy-bandwidth probe")
     args = ap.parse_args()
 
     import torch
@@ -197,22 +255,31 @@ def main():
     if rank == 0:
         ab = algorithmic_bytes(ctr, cfg["levels"])
         roof = None
-        if not args.no_timing and ktimes["tile"][1] > 0:
+        if not args.no_timing and ktimes["update"][1] > 0:
             dom = max(KERNELS, key=lambda k: ktimes[k][0])
             ms, nlaunch = ktimes[dom]
             per_launch_bytes = ab[dom] / nlaunch
             avg_s = ms / 1e3 / nlaunch
             achieved = per_launch_bytes / avg_s / 1e9
-            roof = {"bound": "hbm", "kernel": f"hs_{dom}_kernel", "achieved": round(achieved, 2),
+            ksym = kernel_symbol(dom, ktimes)
+            pmc = pmc_traffic(ksym, args.config, B)
+            roof = {"bound": "hbm", "kernel": ksym, "achieved": round(achieved, 2),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                    "traffic": None, "avg_launch_ms": round(ms / nlaunch, 5),
+                    "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
+                    "traffic_source": (f"{pmc['source']} (FETCH_SIZE x2 + WRITE_SIZE)" if pmc else None),
+                    "traffic_GBps": (round(pmc["traffic_bytes_per_launch"] / avg_s / 1e9, 2) if pmc else None),
+                    "min_traffic_per_launch": (int(ctr["touched"] * 12 / nlaunch) if dom == "update" else None),
+                    "avg_launch_ms": round(ms / nlaunch, 5),
                     "alg_bytes_per_launch": int(per_launch_bytes),
                     "kernel_ms_per_step": {k: round(ktimes[k][0] / max(ktimes[k][1], 1), 5) for k in KERNELS},
                     "whole_step_GBps": round(ab["total"] / K / (t_max / K) / 1e9, 2),
                     "whole_step_frac": round(ab["total"] / t_max / 1e9 / HBM_PEAK_GBS, 5),
                     "read_only_frac": round(ab["read_only"] / t_max / 1e9 / HBM_PEAK_GBS, 5),
                     "alg_bytes_per_scan": int(ab["total"] / max(B * K, 1)),
-                    "cells_per_scan": round(ctr["cells"] / max(B * K, 1), 1)}
+                    "cells_per_scan": round(ctr["cells"] / max(B * K, 1), 1),
+                    "distinct_cells_per_scan": round(ctr["touched"] / max(B * K, 1), 1)}
+            if not args.no_copy_probe:
+                roof["attainable_copy_GBps"] = round(copy_bandwidth(dev), 1)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg)

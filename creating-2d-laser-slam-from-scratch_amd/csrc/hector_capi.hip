@@ -38,6 +38,7 @@ int fail(int code, const char *what, hipError_t e = hipSuccess)
     } while (0)
 
 constexpr int NKERN = 3;
+constexpr int MAX_PARTS = 4;
 
 struct EventPair {
     hipEvent_t a, b;
@@ -72,9 +73,15 @@ struct hs_ctx {
     uint4 *d_segs = nullptr;
     WorkItem *d_items = nullptr;
     WorkItem *d_wholes = nullptr;
-    WorkQueue *d_wq = nullptr;
-    unsigned seg_cap = 0, item_cap = 0;
+    WorkQueue *d_wq = nullptr;  // one queue per part
+    unsigned seg_cap = 0, item_cap = 0;  // per part
     int tile_grid = 0;
+    // batch split into parts on separate HIP streams so one part's tile kernel overlaps another
+    // part's match / bin kernels (they are latency-bound at low occupancy)
+    int nparts = 1;
+    int update_single = 1;  // hs_update_kernel (per stream-level, default) or bin + tile kernels
+    hipStream_t pstream[MAX_PARTS] = {};
+    hipEvent_t ev_start = nullptr, ev_done[MAX_PARTS] = {};
 };
 
 namespace {
@@ -173,26 +180,63 @@ void end_timed(hs_ctx *c, hipStream_t s)
     hipEventRecord(c->ev_used.back().b, s);
 }
 
-int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride, const int *n, const float2 *origo,
-                const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s)
+int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int xy_stride, const int *n,
+                const float2 *origo, const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s)
 {
-    if (count <= 0) return HS_OK;
+    WorkQueue *wq = c->d_wq + part;
+    uint4 *segs = c->d_segs + (size_t)part * c->seg_cap;
+    WorkItem *items = c->d_items + (size_t)part * c->item_cap;
+    WorkItem *wholes = c->d_wholes + (size_t)part * c->B * c->levels;
     begin_timed(c, 0, s);
     hipLaunchKernelGGL(hs_match_kernel, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state, xy,
-                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, c->d_wq);
+                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq);
     end_timed(c, s);
     HCHK(hipGetLastError());
     if (mode == MODE_MATCH_ONLY) return HS_OK;
+    if (c->update_single) {
+        const size_t shmem = sizeof(unsigned) * (2 * (size_t)TILE_CELLS + (size_t)c->max_points);
+        begin_timed(c, 2, s);
+        hipLaunchKernelGGL(hs_update_kernel, dim3(count * c->levels), dim3(UPD_THREADS), shmem, s, c->geom, c->d_cells,
+                           c->d_state, xy, xy_stride, begin, count, c->max_points);
+        end_timed(c, s);
+        HCHK(hipGetLastError());
+        return HS_OK;
+    }
     begin_timed(c, 1, s);
     hipLaunchKernelGGL(hs_bin_kernel, dim3(count), dim3(BIN_THREADS), 0, s, c->geom, c->d_state, xy, xy_stride, begin,
-                       c->max_points, c->d_rays, c->d_segs, c->d_items, c->d_wholes, c->d_wq, c->seg_cap, c->item_cap);
+                       c->max_points, c->d_rays, segs, items, wholes, wq, c->seg_cap, c->item_cap);
     end_timed(c, s);
     HCHK(hipGetLastError());
     begin_timed(c, 2, s);
     hipLaunchKernelGGL(hs_tile_kernel, dim3(c->tile_grid), dim3(TILE_THREADS), 0, s, c->geom, c->d_cells, c->d_state,
-                       c->d_rays, c->d_segs, c->d_items, c->d_wholes, c->d_wq, c->max_points);
+                       c->d_rays, segs, items, wholes, wq, c->max_points);
     end_timed(c, s);
     HCHK(hipGetLastError());
+    return HS_OK;
+}
+
+int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride, const int *n, const float2 *origo,
+                const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s)
+{
+    if (count <= 0) return HS_OK;
+    const int parts = (mode == MODE_PROCESS && count >= 64 * c->nparts) ? c->nparts : 1;
+    if (parts == 1) return launch_part(c, 0, begin, count, xy, xy_stride, n, origo, hints, mode, out_pose, out_cov, s);
+    HCHK(hipEventRecord(c->ev_start, s));
+    const int per = (count + parts - 1) / parts;
+    for (int p = 0; p < parts; ++p) {
+        const int off = p * per;
+        const int cnt = count - off < per ? count - off : per;
+        if (cnt <= 0) break;
+        hipStream_t ps = c->pstream[p];
+        HCHK(hipStreamWaitEvent(ps, c->ev_start, 0));
+        int rc = launch_part(c, p, begin + off, cnt, xy + (size_t)off * xy_stride, xy_stride, n + off,
+                             origo ? origo + off : nullptr, hints ? hints + 3 * (size_t)off : nullptr, mode,
+                             out_pose ? out_pose + 3 * (size_t)off : nullptr, out_cov ? out_cov + 9 * (size_t)off : nullptr,
+                             ps);
+        if (rc != HS_OK) return rc;
+        HCHK(hipEventRecord(c->ev_done[p], ps));
+        HCHK(hipStreamWaitEvent(s, c->ev_done[p], 0));
+    }
     return HS_OK;
 }
 
@@ -267,9 +311,6 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         size_t segs = sl * (size_t)max_points * 6, its = sl * 512;
         if (segs < (1u << 20)) segs = 1u << 20;
         if (its < (1u << 14)) its = 1u << 14;
-        // test hook: shrink the queues to exercise the WHOLE (unbinned) fallback
-        if (const char *e = getenv("SLAM2D_SEG_CAP")) segs = (size_t)atoll(e);
-        if (const char *e = getenv("SLAM2D_ITEM_CAP")) its = (size_t)atoll(e);
         c->seg_cap = (unsigned)(segs < 0xFFFFFFF0ull ? segs : 0xFFFFFFF0ull);
         c->item_cap = (unsigned)(its < 0xFFFFFFF0ull ? its : 0xFFFFFFF0ull);
         int dev = 0, ncu = 256;
@@ -282,12 +323,34 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
             per_cu = 4;
         const char *tg = getenv("SLAM2D_TILE_WG_PER_CU");
         c->tile_grid = ncu * (tg ? atoi(tg) : per_cu);
+        const char *np = getenv("SLAM2D_PARTS");
+        c->nparts = np ? atoi(np) : 1;
+        const char *um = getenv("SLAM2D_UPDATE");
+        c->update_single = (um && strcmp(um, "binned") == 0) ? 0 : 1;  // measured: single 1.06 ms vs binned 1.30 ms
+        if (c->nparts < 1) c->nparts = 1;
+        if (c->nparts > MAX_PARTS) c->nparts = MAX_PARTS;
+        // per-part capacities (test hooks SLAM2D_SEG_CAP / SLAM2D_ITEM_CAP set them directly)
+        if (const char *e2 = getenv("SLAM2D_SEG_CAP")) c->seg_cap = (unsigned)atoll(e2);
+        else c->seg_cap = (unsigned)((size_t)c->seg_cap / c->nparts + (1u << 16));
+        if (const char *e2 = getenv("SLAM2D_ITEM_CAP")) c->item_cap = (unsigned)atoll(e2);
+        else c->item_cap = (unsigned)((size_t)c->item_cap / c->nparts + (1u << 10));
+        for (int p = 0; p < c->nparts; ++p) {
+            if ((e = hipStreamCreateWithFlags(&c->pstream[p], hipStreamNonBlocking)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&c->ev_done[p], hipEventDisableTiming)) != hipSuccess) {
+                hs_destroy(c);
+                return fail(HS_EHIP, "hipStreamCreate(part)", e);
+            }
+        }
+        if ((e = hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming)) != hipSuccess) {
+            hs_destroy(c);
+            return fail(HS_EHIP, "hipEventCreate", e);
+        }
     }
     if ((e = hipMalloc(&c->d_rays, sizeof(unsigned) * (size_t)num_streams * levels * max_points)) != hipSuccess ||
-        (e = hipMalloc(&c->d_segs, sizeof(uint4) * (size_t)c->seg_cap)) != hipSuccess ||
-        (e = hipMalloc(&c->d_items, sizeof(WorkItem) * (size_t)c->item_cap)) != hipSuccess ||
-        (e = hipMalloc(&c->d_wholes, sizeof(WorkItem) * (size_t)num_streams * levels)) != hipSuccess ||
-        (e = hipMalloc(&c->d_wq, sizeof(WorkQueue))) != hipSuccess) {
+        (e = hipMalloc(&c->d_segs, sizeof(uint4) * (size_t)c->seg_cap * c->nparts)) != hipSuccess ||
+        (e = hipMalloc(&c->d_items, sizeof(WorkItem) * (size_t)c->item_cap * c->nparts)) != hipSuccess ||
+        (e = hipMalloc(&c->d_wholes, sizeof(WorkItem) * (size_t)num_streams * levels * c->nparts)) != hipSuccess ||
+        (e = hipMalloc(&c->d_wq, sizeof(WorkQueue) * c->nparts)) != hipSuccess) {
         hs_destroy(c);
         return fail(HS_ENOMEM, "hipMalloc", e);
     }
@@ -296,9 +359,11 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         memset(&q, 0, sizeof(q));
         q.item_cap = c->item_cap;
         q.seg_cap = c->seg_cap;
-        if ((e = hipMemcpy(c->d_wq, &q, sizeof(q), hipMemcpyHostToDevice)) != hipSuccess) {
-            hs_destroy(c);
-            return fail(HS_EHIP, "hipMemcpy(work queue)", e);
+        for (int p = 0; p < c->nparts; ++p) {
+            if ((e = hipMemcpy(c->d_wq + p, &q, sizeof(q), hipMemcpyHostToDevice)) != hipSuccess) {
+                hs_destroy(c);
+                return fail(HS_EHIP, "hipMemcpy(work queue)", e);
+            }
         }
     }
     int rc = reset_all(c);
@@ -336,6 +401,11 @@ int hs_destroy(hs_ctx *c)
         hipEventDestroy(p.a);
         hipEventDestroy(p.b);
     }
+    for (int p = 0; p < MAX_PARTS; ++p) {
+        if (c->pstream[p]) hipStreamDestroy(c->pstream[p]);
+        if (c->ev_done[p]) hipEventDestroy(c->ev_done[p]);
+    }
+    if (c->ev_start) hipEventDestroy(c->ev_start);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return HS_OK;
@@ -531,22 +601,24 @@ int hs_get_poses(hs_ctx *c, float *poses_out, float *covs_out, int *did_update_o
     return HS_OK;
 }
 
-int hs_get_counters(hs_ctx *c, int64_t out[5], int reset)
+int hs_get_counters(hs_ctx *c, int64_t out[6], int reset)
 {
     if (!c || !out) return fail(HS_EINVAL, "NULL argument");
     std::vector<StreamState> h(c->B);
     HCHK(hipStreamSynchronize(c->stream));
     HCHK(hipDeviceSynchronize());
     HCHK(hipMemcpy(h.data(), c->d_state, sizeof(StreamState) * c->B, hipMemcpyDeviceToHost));
-    for (int k = 0; k < 5; ++k) out[k] = 0;
+    for (int k = 0; k < 6; ++k) out[k] = 0;
     for (int s = 0; s < c->B; ++s) {
         out[0] += (int64_t)h[s].tot_cells;
         out[1] += (int64_t)h[s].tot_rays;
         out[2] += (int64_t)h[s].tot_gn_points;
         out[3] += (int64_t)h[s].tot_updates;
         out[4] += (int64_t)h[s].tot_steps;
+        out[5] += (int64_t)h[s].tot_touched;
         if (reset) {
             h[s].tot_cells = h[s].tot_rays = h[s].tot_gn_points = h[s].tot_updates = h[s].tot_steps = 0;
+            h[s].tot_touched = 0;
         }
     }
     if (reset) HCHK(hipMemcpy(c->d_state, h.data(), sizeof(StreamState) * c->B, hipMemcpyHostToDevice));
@@ -556,15 +628,18 @@ int hs_get_counters(hs_ctx *c, int64_t out[5], int reset)
 int hs_get_queue_stats(hs_ctx *c, int64_t out[8], int reset_stamps)
 {
     if (!c || !out) return fail(HS_EINVAL, "NULL argument");
-    WorkQueue q;
+    WorkQueue q[MAX_PARTS];
     unsigned long long st[8];
     HCHK(hipDeviceSynchronize());
-    HCHK(hipMemcpy(&q, c->d_wq, sizeof(q), hipMemcpyDeviceToHost));
+    HCHK(hipMemcpy(q, c->d_wq, sizeof(WorkQueue) * c->nparts, hipMemcpyDeviceToHost));
     HCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
-    out[0] = q.item_used;
-    out[1] = q.seg_used;
-    out[2] = q.whole_used;
-    out[3] = q.overflow;
+    for (int k = 0; k < 4; ++k) out[k] = 0;
+    for (int p = 0; p < c->nparts; ++p) {
+        out[0] += q[p].item_used;
+        out[1] += q[p].seg_used;
+        out[2] += q[p].whole_used;
+        out[3] += q[p].overflow;
+    }
     for (int k = 0; k < 4; ++k) out[4 + k] = (int64_t)st[k];
     if (reset_stamps) {
         memset(st, 0, sizeof(st));

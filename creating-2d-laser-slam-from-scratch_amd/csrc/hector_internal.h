@@ -81,6 +81,7 @@ struct alignas(16) StreamState {
     unsigned long long tot_gn_points; // Σ over GN iterations of the points evaluated
     unsigned long long tot_updates;   // map updates (steps with do_update)
     unsigned long long tot_steps;     // steps
+    unsigned long long tot_touched;   // distinct cells written by the grid update (Σ levels, per scan)
     int step_index;                   // steps since hs_reset (pose-log row)
     int pad_;
 };

@@ -846,6 +846,7 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
                 sg_nxt = segs[nxt.seg_begin + lane];
             S2D_STAMP(tc);
             if (__any(any)) {
+                unsigned touched = 0;
                 // apply: lane = column -> 256 B / 512 B coalesced row accesses
 #pragma unroll
                 for (int row = 0; row < TILE_H; ++row) {
@@ -875,7 +876,12 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
                     tl[row * TILE + lane] = l;
                     tu[row * TILE + lane] = upd;
 #endif
+                    ++touched;
                 }
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);
+                if (lane == 0 && touched)
+                    atomicAdd(&const_cast<StreamState *>(state)[s].tot_touched, (unsigned long long)touched);
             }
             ++gen;
             S2D_STAMP(td);
@@ -900,6 +906,182 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
     (void)ts0; (void)acc0; (void)acc1; (void)acc2; (void)ntiles; (void)tb; (void)tc; (void)td;
 #endif
 }
+
+// ------------------------------------------------- k2 (default): per-(stream, level) grid update
+// Default update path (SLAM2D_UPDATE=binned selects k2/k3 above).  One workgroup per (stream, level),
+// rays resident in LDS; for
+// each 64 x TILE_H tile of the scan's bounding box:
+//   (1) every ray's end cell in the tile: LDS atomicMin(first_hit, beam); every free step of the
+//       ray inside the tile (closed-form step range): LDS atomicMin(first_free, beam) -- blind
+//       atomics, no read-modify-write chain, one barrier;
+//   (2) one coalesced read-modify-write of every touched cell (8 B) applying the reference's
+//       float sequence: free only: l + lf; hit: ((l + lf) - lf) if freed first, then + lo if < 50.
+// This equals running bresenhamCellFree / bresenhamCellOcc (:302-330) beam by beam.
+#ifndef S2D_APPLY_BATCH
+#define S2D_APPLY_BATCH 8
+#endif
+__global__ void __launch_bounds__(UPD_THREADS)
+hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restrict__ state,
+                 const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned smem[];
+    unsigned *first_hit = smem;                    // TILE_CELLS words
+    unsigned *first_free = smem + TILE_CELLS;      // TILE_CELLS words
+    unsigned *rays = smem + 2 * TILE_CELLS;        // max_points packed end cells
+    __shared__ int s_bbox[4];
+
+    // level-major block order: every stream's level 0 (the largest) is dispatched first
+    const int lvl = blockIdx.x / count;
+    const int local = blockIdx.x - lvl * count;
+    const int s = stream_begin + local;
+    const StreamState &st = state[s];
+    if (!st.do_update) return;
+    const LevelGeom &g = geom.lv[lvl];
+    const int n = st.n;
+    const int tid = threadIdx.x;
+    float *lvw = cells + (size_t)s * geom.stream_words + g.word_offset;
+
+    const RayFrame fr = ray_frame(g, st);
+    const int x0 = fr.bxi, y0 = fr.byi;
+    if (tid == 0) {
+        s_bbox[0] = x0; s_bbox[1] = y0; s_bbox[2] = x0; s_bbox[3] = y0;
+    }
+    __syncthreads();
+    int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
+    unsigned long long L = 0, R = 0;
+    const float2 *pts = xy + (size_t)local * xy_stride;
+    for (int b = tid; b < n; b += UPD_THREADS) {
+        unsigned r = make_ray(g, fr, pts[b]);
+        rays[b] = r;
+        if (r != RAY_INVALID) {
+            int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+            bx0 = min(bx0, x1); by0 = min(by0, y1); bx1 = max(bx1, x1); by1 = max(by1, y1);
+            int adx = abs(x1 - x0), ady = abs(y1 - y0);
+            L += (unsigned long long)(max(adx, ady) + 1);
+            R += 1;
+        }
+    }
+    if (R) {
+        atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
+        atomicMax(&s_bbox[2], bx1); atomicMax(&s_bbox[3], by1);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        L += __shfl_xor(L, off, 64);
+        R += __shfl_xor(R, off, 64);
+    }
+    if ((tid & 63) == 0 && R) {
+        atomicAdd(&state[s].step_cells, L);
+        atomicAdd(&state[s].tot_cells, L);
+        atomicAdd(&state[s].tot_rays, R);
+    }
+    if (!__syncthreads_or(R != 0)) return;  // no ray drawn on this level
+    const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / TILE_H;
+    const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / TILE_H;
+    const int mark_free = st.mark_base + 1;  // currMarkFreeIndex (:120)
+    const int mark_occ = st.mark_base + 2;   // currMarkOccIndex  (:121)
+    const float lf = geom.lf, lo = geom.lo;
+    unsigned touched = 0;
+
+    for (int ty = ty0; ty <= ty1; ++ty) {
+        for (int tx = tx0; tx <= tx1; ++tx) {
+            const int X0 = tx * TILE, Y0 = ty * TILE_H;
+            const int X1 = X0 + TILE, Y1 = Y0 + TILE_H;
+            for (int k = tid; k < 2 * TILE_CELLS / 4; k += UPD_THREADS)
+                reinterpret_cast<uint4 *>(smem)[k] = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
+            __syncthreads();
+            bool any = false;
+            for (int b = tid; b < n; b += UPD_THREADS) {
+                unsigned r = rays[b];
+                if (r == RAY_INVALID) continue;
+                int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+                if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
+                if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {
+                    atomicMin(&first_hit[(y1 - Y0) * TILE + (x1 - X0)], (unsigned)b);  // bresenhamCellOcc (:266)
+                    any = true;
+                }
+                RayWalk w = ray_walk(x0, y0, x1, y1);
+                int lo_i, hi_i;
+                bool in = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i) : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
+                if (!in) continue;
+                if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
+                if (lo_i > hi_i) continue;
+                any = true;
+                const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
+                const int q = (int)(num / (unsigned)w.da);
+                int err = (int)(num - (unsigned)q * (unsigned)w.da);
+                // local LDS index of step lo_i and its increments along the major / minor axis
+                const int la = w.x_major ? 1 : TILE;
+                const int lb = w.x_major ? TILE : 1;
+                const int ax = w.a0 + w.sa * lo_i - (w.x_major ? X0 : Y0);
+                const int bx = w.b0 + w.sb * q - (w.x_major ? Y0 : X0);
+                int li = ax * la + bx * lb;
+                const int da_step = w.sa * la, db_step = w.sb * lb;
+                for (int i = lo_i; i <= hi_i; ++i) {
+                    atomicMin(&first_free[li], (unsigned)b);  // bresenhamCellFree (:302-312)
+                    li += da_step;
+                    err += w.db;
+                    if (err >= w.da) {
+                        err -= w.da;
+                        li += db_step;
+                    }
+                }
+            }
+            if (!__syncthreads_or(any)) continue;
+            // apply: wave w handles rows w, w+4, ...; lane = column -> 512 B coalesced rows;
+            // the loads of a batch of rows are issued before any store of that batch.
+            const int col = tid & 63;
+            const int gx = X0 + col;
+            float *tl = lvw + (size_t)(tx + ty * g.tiles_x) * TILE_BLOCK_WORDS;
+            int *tu = reinterpret_cast<int *>(tl + TILE_CELLS);
+            constexpr int RPW = TILE_H / (UPD_THREADS / 64);  // rows per wave
+            constexpr int NB = S2D_APPLY_BATCH < RPW ? S2D_APPLY_BATCH : RPW;
+#pragma unroll
+            for (int k0 = 0; k0 < RPW; k0 += NB) {
+                unsigned fh[NB], ff[NB];
+                float cv[NB];
+#pragma unroll
+                for (int k = 0; k < NB; ++k) {
+                    const int row = (tid >> 6) + (k0 + k) * (UPD_THREADS / 64);
+                    const int gy = Y0 + row;
+                    unsigned h = first_hit[row * TILE + col];
+                    unsigned f = first_free[row * TILE + col];
+                    if (gx >= g.sx || gy >= g.sy) h = f = W_NONE;
+                    fh[k] = h;
+                    ff[k] = f;
+                    if ((h & f) != W_NONE) cv[k] = tl[row * TILE + col];
+                }
+#pragma unroll
+                for (int k = 0; k < NB; ++k) {
+                    const unsigned h = fh[k], f = ff[k];
+                    if ((h & f) == W_NONE) continue;
+                    const int row = (tid >> 6) + (k0 + k) * (UPD_THREADS / 64);
+                    float l = cv[k];
+                    int upd;
+                    if (h == W_NONE) {
+                        l = l + lf;        // updateSetFree (GridMapLogOdds.h:120-124)
+                        upd = mark_free;
+                    } else {
+                        if (f < h) {
+                            l = l + lf;    // bresenhamCellFree by an earlier beam
+                            l = l - lf;    // updateUnsetFree (GridMapLogOdds.h:126-129)
+                        }
+                        if (l < 50.0f) l = l + lo;  // updateSetOccupied (:108-114)
+                        upd = mark_occ;
+                    }
+                    tl[row * TILE + col] = l;
+                    tu[row * TILE + col] = upd;
+                    ++touched;
+                }
+            }
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);
+    if ((tid & 63) == 0 && touched) atomicAdd(&state[s].tot_touched, (unsigned long long)touched);
+}
+
 
 // --------------------------------------------------------------------------- utility kernels
 __global__ void hs_fill_cells_kernel(float *__restrict__ words, size_t n)

@@ -199,9 +199,10 @@ class HectorFleet:
         return p, cv.reshape(self.B, 3, 3), d.astype(bool), cells
 
     def counters(self, reset=True):
-        o = np.zeros(5, np.int64)
+        o = np.zeros(6, np.int64)
         check(self.L.hs_get_counters(self.h, _fp(o), 1 if reset else 0), "hs_get_counters")
-        return {"cells": int(o[0]), "rays": int(o[1]), "gn_points": int(o[2]), "updates": int(o[3]), "steps": int(o[4])}
+        return {"cells": int(o[0]), "rays": int(o[1]), "gn_points": int(o[2]), "updates": int(o[3]), "steps": int(o[4]),
+                "touched": int(o[5])}
 
     def set_pose_log(self, d_buf: int, streams: int, capacity: int):
         """Device pose log (float32 [capacity][streams][3]) filled by every step; d_buf = 0 disables."""
@@ -223,7 +224,7 @@ class HectorFleet:
         ms = np.zeros(3, np.float64)
         n = np.zeros(3, np.int64)
         check(self.L.hs_get_kernel_times(self.h, _fp(ms), _fp(n), 1 if reset else 0), "hs_get_kernel_times")
-        names = ("match", "bin", "tile")
+        names = ("match", "bin", "update")  # slot 2: hs_update_kernel (default) or hs_tile_kernel (binned)
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}
 
 

@@ -103,8 +103,10 @@ int hs_step_batch_device(hs_ctx *ctx, int stream_begin, int count, const float *
 int hs_get_poses(hs_ctx *ctx, float *poses_out, float *covs_out, int *did_update_out, int64_t *cells_traversed_out);
 /* Cumulative work counters summed over streams since the last reset (synchronises):
  * out[0] Σ cells traversed (Σ abs_da+1), out[1] valid rays, out[2] Σ points x GN iterations,
- * out[3] map updates, out[4] steps.  reset != 0 zeroes them afterwards. */
-int hs_get_counters(hs_ctx *ctx, int64_t out[5], int reset);
+ * out[3] map updates, out[4] steps, out[5] distinct cells written by the grid update (each is
+ * one 4 B log-odds read + 8 B write: the minimum HBM traffic of the update).  reset != 0 zeroes
+ * them afterwards. */
+int hs_get_counters(hs_ctx *ctx, int64_t out[6], int reset);
 /* Grid-update queue of the last step: out[0] tile work items, out[1] ray segments, out[2] WHOLE
  * (unbinned) level items, out[3] overflow events (cumulative); out[4..7] diagnostic-build phase
  * cycle sums of hs_tile_kernel (setup+clear, raster, apply, tiles; zero in normal builds). */

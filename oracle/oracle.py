@@ -42,13 +42,13 @@ def _fp(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-_HL = None
+_HL = {}
 
 
-def hector_lib() -> C.CDLL:
-    global _HL
-    if _HL is None:
-        L = _lib(os.path.join(BUILD, "libhector_oracle.so"))
+def hector_lib(variant: str = "") -> C.CDLL:
+    """variant "" = -O3 build, "O0" = the -O0 build (CPU-baseline comparison only)."""
+    if variant not in _HL:
+        L = _lib(os.path.join(BUILD, f"libhector_oracle{'_' + variant if variant else ''}.so"))
         L.ho_create.restype = _p
         L.ho_create.argtypes = [_f, _i, _i, _f, _f, _i]
         L.ho_destroy.argtypes = [_p]
@@ -83,8 +83,8 @@ def hector_lib() -> C.CDLL:
         for n in ("ho_det_sinf", "ho_det_cosf", "ho_det_expf"):
             getattr(L, n).restype = _f
             getattr(L, n).argtypes = [_f]
-        _HL = L
-    return _HL
+        _HL[variant] = L
+    return _HL[variant]
 
 
 class HectorOracle:
@@ -95,8 +95,8 @@ class HectorOracle:
     """
 
     def __init__(self, map_resolution=0.05, map_size=1024, start=(0.5, 0.5), levels=1, reduce_threads=0,
-                 use_libm=False, map_size_y=None):
-        self.L = hector_lib()
+                 use_libm=False, map_size_y=None, lib_variant=""):
+        self.L = hector_lib(lib_variant)
         sy = map_size if map_size_y is None else map_size_y
         self.h = self.L.ho_create(_f(map_resolution), map_size, sy, _f(start[0]), _f(start[1]), levels)
         if not self.h:

@@ -79,15 +79,20 @@ def test_out_of_map_beams_small_map(gpu, scans):
 
 @pytest.mark.parametrize("cap_env", ["SLAM2D_SEG_CAP", "SLAM2D_ITEM_CAP"])
 def test_unbinned_fallback_bitexact(gpu, scans, monkeypatch, cap_env):
-    """Queue overflow -> WHOLE items (every ray tested against every tile of the level's bbox)."""
+    """Binned path, queue overflow -> WHOLE items (every ray against every tile of the level's bbox)."""
+    monkeypatch.setenv("SLAM2D_UPDATE", "binned")
     monkeypatch.setenv(cap_env, "8")
     fleet, _ = _run_pair(2, 1024, scans, n_scans=8, thresholds=(-1.0, -1.0), stream=2)
     q = fleet.queue_stats()
     assert q["whole"] > 0 and q["overflow"] > 0, q
 
 
-def test_binned_path_used(gpu, scans):
-    fleet, _ = _run_pair(3, 1024, scans, n_scans=3, thresholds=(-1.0, -1.0))
+@pytest.mark.parametrize("parts", ["1", "2"])
+def test_binned_path_bitexact(gpu, scans, monkeypatch, parts):
+    """Alternative update path: hs_bin_kernel + hs_tile_kernel (SLAM2D_UPDATE=binned)."""
+    monkeypatch.setenv("SLAM2D_UPDATE", "binned")
+    monkeypatch.setenv("SLAM2D_PARTS", parts)
+    fleet, _ = _run_pair(3, 2048, scans, n_scans=10, thresholds=(-1.0, -1.0), stream=1)
     q = fleet.queue_stats()
     assert q["whole"] == 0 and q["overflow"] == 0 and q["items"] > 0, q
 

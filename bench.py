@@ -80,6 +80,20 @@ def pmc_traffic(kernel: str, cfg_name: str, streams: int):
     return None
 
 
+def aggregate_over_ranks(elapsed: float, units: float, device):
+    """Whole-job timing: the slowest rank's time (MAX) and the units all ranks processed (SUM).
+    Works on any backend (RCCL on the GPU box, gloo in the CPU tests)."""
+    import torch
+    import torch.distributed as dist
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    un = torch.tensor([units], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(un, op=dist.ReduceOp.SUM)
+    return float(el.item()), float(un.item())
+
+
 def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
     """Attainable device-to-device copy bandwidth (read + write bytes / time), torch copy_."""
     import torch
@@ -243,13 +257,7 @@ def main():
     ktimes = fleet.kernel_times(reset=True)
     ctr = fleet.counters(reset=True)
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    scans = torch.tensor([float(B * K)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        dist.all_reduce(scans, op=dist.ReduceOp.SUM)
-    t_max = float(el.item())
-    total_scans = float(scans.item())
+    t_max, total_scans = aggregate_over_ranks(elapsed, float(B * K), dev)
     value = total_scans / t_max
 
     if rank == 0:

@@ -193,10 +193,15 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     end_timed(c, s);
     HCHK(hipGetLastError());
     if (mode == MODE_MATCH_ONLY) return HS_OK;
-    if (c->update_single) {
-        const size_t shmem = sizeof(unsigned) * (2 * (size_t)TILE_CELLS + (size_t)c->max_points);
+    // hs_update_kernel keeps the scan's rays in LDS: beyond 64 KB of dynamic LDS (max_points > ~11k)
+    // the binned kernels, whose LDS use is independent of the scan size, take over
+    const size_t upd_shmem = sizeof(unsigned) * (2 * (size_t)UPD_TILE_WORDS + (size_t)((c->max_points + 3) & ~3) +
+                                                 4 * (size_t)((c->max_points + 63) / 64));
+    if (c->update_single && upd_shmem <= 65536) {
         begin_timed(c, 2, s);
-        hipLaunchKernelGGL(hs_update_kernel, dim3(count * c->levels), dim3(UPD_THREADS), shmem, s, c->geom, c->d_cells,
+        int blocks = 0;
+        for (int l = 0; l < c->levels; ++l) blocks += c->geom.upd_parts[l] * count;
+        hipLaunchKernelGGL(hs_update_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
                            c->d_state, xy, xy_stride, begin, count, c->max_points);
         end_timed(c, s);
         HCHK(hipGetLastError());
@@ -327,6 +332,19 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         c->nparts = np ? atoi(np) : 1;
         const char *um = getenv("SLAM2D_UPDATE");
         c->update_single = (um && strcmp(um, "binned") == 0) ? 0 : 1;  // measured: single 1.06 ms vs binned 1.30 ms
+        // workgroups per (stream, level) of hs_update_kernel: 1 (splitting a level's tiles over more
+        // workgroups measured slower: each part redoes the ray setup); SLAM2D_UPD_PARTS="p0,p1,..." 
+        for (int l = 0; l < MAX_LEVELS; ++l) c->geom.upd_parts[l] = 1;
+        if (const char *up = getenv("SLAM2D_UPD_PARTS")) {
+            int l = 0;
+            for (const char *q = up; *q && l < MAX_LEVELS; ++l) {
+                const int v = atoi(q);
+                c->geom.upd_parts[l] = v < 1 ? 1 : (v > 64 ? 64 : v);
+                while (*q && *q != ',') ++q;
+                if (*q == ',') ++q;
+            }
+            for (; l < MAX_LEVELS; ++l) c->geom.upd_parts[l] = c->geom.upd_parts[l - 1];
+        }
         if (c->nparts < 1) c->nparts = 1;
         if (c->nparts > MAX_PARTS) c->nparts = MAX_PARTS;
         // per-part capacities (test hooks SLAM2D_SEG_CAP / SLAM2D_ITEM_CAP set them directly)

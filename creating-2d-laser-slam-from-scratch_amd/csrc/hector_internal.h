@@ -58,6 +58,7 @@ struct FleetGeom {
     float lf, lo;              // logOddsFree / logOddsOccupied
     float min_dist, min_ang;   // map update thresholds
     size_t stream_words;       // 4-byte words per stream (all levels, tiled, both planes)
+    int upd_parts[MAX_LEVELS]; // hs_update_kernel workgroups per (stream, level)
     LevelGeom lv[MAX_LEVELS];
 };
 

@@ -108,7 +108,7 @@ __device__ __forceinline__ void point_terms(const float *__restrict__ lvl_words,
     float x = tx + (cs * px + nsn * py);
     float y = ty + (sn * px + cs * py);
     float v, gx, gy;
-    if ((x < 0.0f) || (x > g.lim[0]) || (y < 0.0f) || (y > g.lim[1])) {
+    if (!(x >= 0.0f) || !(x <= g.lim[0]) || !(y >= 0.0f) || !(y <= g.lim[1])) {  // NaN -> out of map
         v = 0.0f;
         gx = 0.0f;
         gy = 0.0f;
@@ -330,6 +330,13 @@ constexpr int UPD_THREADS = 256;
 // first (first_free < first_hit) ((l + lf) - lf), then + lo if l < 50.
 constexpr unsigned W_NONE = 0xFFFFFFFFu;
 
+// (int)v of :135/:154 for v in int range; NaN / out of range -> -1 (cancelled by the bounds check,
+// as x86's INT_MIN is in the reference; the GPU's saturating convert would turn NaN into cell 0)
+__device__ __forceinline__ int cell_of(float v)
+{
+    return (v > -2147483648.0f && v < 2147483648.0f) ? (int)v : -1;
+}
+
 struct RayFrame {
     float mx, my, cs, sn;
     int bxi, byi;
@@ -349,8 +356,8 @@ __device__ __forceinline__ RayFrame ray_frame(const LevelGeom &g, const StreamSt
     float nsn = -fr.sn;
     float bx = fr.mx + (fr.cs * ox + nsn * oy);   // poseTransform * origo (:132)
     float by = fr.my + (fr.sn * ox + fr.cs * oy);
-    fr.bxi = (int)(bx + 0.5f);                     // (:135)
-    fr.byi = (int)(by + 0.5f);
+    fr.bxi = cell_of(bx + 0.5f);                   // (:135)
+    fr.byi = cell_of(by + 0.5f);
     return fr;
 }
 
@@ -363,7 +370,7 @@ __device__ __forceinline__ unsigned make_ray(const LevelGeom &g, const RayFrame 
     float ey = fr.my + (fr.sn * px + fr.cs * py);
     ex += 0.5f;                                   // (:151)
     ey += 0.5f;
-    int x1 = (int)ex, y1 = (int)ey;               // (:154)
+    int x1 = cell_of(ex), y1 = cell_of(ey);       // (:154)
     int x0 = fr.bxi, y0 = fr.byi;
     if (x0 == x1 && y0 == y1) return RAY_INVALID;
     if ((x0 < 0) || (x0 >= g.sx) || (y0 < 0) || (y0 >= g.sy)) return RAY_INVALID;
@@ -908,31 +915,74 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
 }
 
 // ------------------------------------------------- k2 (default): per-(stream, level) grid update
-// Default update path (SLAM2D_UPDATE=binned selects k2/k3 above).  One workgroup per (stream, level),
-// rays resident in LDS; for
-// each 64 x TILE_H tile of the scan's bounding box:
-//   (1) every ray's end cell in the tile: LDS atomicMin(first_hit, beam); every free step of the
-//       ray inside the tile (closed-form step range): LDS atomicMin(first_free, beam) -- blind
-//       atomics, no read-modify-write chain, one barrier;
-//   (2) one coalesced read-modify-write of every touched cell (8 B) applying the reference's
-//       float sequence: free only: l + lf; hit: ((l + lf) - lf) if freed first, then + lo if < 50.
+// Default update path (SLAM2D_UPDATE=binned selects the bin + tile kernels above).  One 256-thread
+// workgroup per (stream, level); the level's rays (packed end cells) stay in LDS.  For each
+// 64 x TILE_H tile of the scan's bounding box:
+//   (1) raster: every ray whose fan group can reach the tile clips itself to the tile (closed-form
+//       Bresenham step range) and marks LDS: atomicMin(first_free, beam) per free step,
+//       atomicMin(first_hit, beam) at its end cell -- blind atomics, no read-modify-write chain;
+//   (2) apply: one coalesced read-modify-write per 4-cell quad holding a mark, applying the
+//       reference's float sequence per cell: free only: l + lf; hit: ((l + lf) - lf) if an earlier
+//       beam freed it, then + lo if l < 50.
 // This equals running bresenhamCellFree / bresenhamCellOcc (:302-330) beam by beam.
-#ifndef S2D_APPLY_BATCH
-#define S2D_APPLY_BATCH 8
+//
+// Fan groups: beams b with the same b / 64 (one wave's lanes in one pass) share a bounding box
+// (origin + their end cells, computed once); a tile outside a group's box is skipped by the whole
+// wave with one scalar test.  Laser scans are angle-ordered, so a group is a narrow fan.
+#ifndef S2D_UPD_STRIDE
+#define S2D_UPD_STRIDE 68
 #endif
+#ifndef S2D_APPLY_UPD_LOAD
+#define S2D_APPLY_UPD_LOAD 1  // 1: updateIndex quads loaded + stored whole; 0: per-cell masked stores
+#endif
+constexpr int UPD_STRIDE = S2D_UPD_STRIDE;            // LDS words per tile row (16-B rows, no 64-stride conflicts)
+constexpr int UPD_TILE_WORDS = TILE_H * UPD_STRIDE;   // one LDS mark array
+static_assert(UPD_STRIDE % 4 == 0 && UPD_STRIDE >= TILE, "quad-aligned LDS rows");
+constexpr int UPD_QUADS = TILE_CELLS / 4 / UPD_THREADS;  // apply quads per thread per tile
+
+// bresenhamCellFree / bresenhamCellOcc outcome of one scan for one cell (h, f: first hitting /
+// freeing beam, W_NONE if none): GridMapLogOddsFunctions (GridMapLogOdds.h:108-129)
+__device__ __forceinline__ int apply_cell(float &l, int &u, unsigned h, unsigned f, float lf, float lo, int mf, int mo)
+{
+    if ((h & f) == W_NONE) return 0;
+    if (h == W_NONE) {
+        l = l + lf;        // updateSetFree (:120-124)
+        u = mf;
+    } else {
+        if (f < h) {
+            l = l + lf;    // bresenhamCellFree by an earlier beam
+            l = l - lf;    // updateUnsetFree (:126-129)
+        }
+        if (l < 50.0f) l = l + lo;  // updateSetOccupied (:108-114)
+        u = mo;
+    }
+    return 1;
+}
+
+__device__ __forceinline__ bool quad_marked(const uint4 &h, const uint4 &f)
+{
+    return ((h.x & f.x) & (h.y & f.y) & (h.z & f.z) & (h.w & f.w)) != W_NONE;
+}
+
+// Grid: for level l, upd_parts[l] x count blocks (level-major, then part, then stream); part p of a
+// level draws the tiles t = p, p + parts, ... of the scan's tile box (t row-major over the box).
 __global__ void __launch_bounds__(UPD_THREADS)
 hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restrict__ state,
                  const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned smem[];
-    unsigned *first_hit = smem;                    // TILE_CELLS words
-    unsigned *first_free = smem + TILE_CELLS;      // TILE_CELLS words
-    unsigned *rays = smem + 2 * TILE_CELLS;        // max_points packed end cells
+    unsigned *first_hit = smem;                        // UPD_TILE_WORDS words
+    unsigned *first_free = smem + UPD_TILE_WORDS;      // UPD_TILE_WORDS words
+    unsigned *rays = smem + 2 * UPD_TILE_WORDS;        // max_points packed end cells
+    int4 *gbox = reinterpret_cast<int4 *>(rays + ((max_points + 3) & ~3));  // per fan group: x0 y0 x1 y1
     __shared__ int s_bbox[4];
 
     // level-major block order: every stream's level 0 (the largest) is dispatched first
-    const int lvl = blockIdx.x / count;
-    const int local = blockIdx.x - lvl * count;
+    int lvl = 0, idx = (int)blockIdx.x;
+    while (lvl + 1 < geom.levels && idx >= geom.upd_parts[lvl] * count) idx -= geom.upd_parts[lvl++] * count;
+    const int parts = geom.upd_parts[lvl];
+    const int part = idx / count;
+    const int local = idx - part * count;
     const int s = stream_begin + local;
     const StreamState &st = state[s];
     if (!st.do_update) return;
@@ -950,16 +1000,30 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
     unsigned long long L = 0, R = 0;
     const float2 *pts = xy + (size_t)local * xy_stride;
-    for (int b = tid; b < n; b += UPD_THREADS) {
-        unsigned r = make_ray(g, fr, pts[b]);
-        rays[b] = r;
+    for (int b0 = tid & ~63; b0 < n; b0 += UPD_THREADS) {   // wave-uniform trip count
+        const int b = b0 + (tid & 63);
+        unsigned r = RAY_INVALID;
+        if (b < n) {
+            r = make_ray(g, fr, pts[b]);
+            rays[b] = r;
+        }
+        int gx0 = x0, gy0 = y0, gx1 = x0, gy1 = y0;  // fan group box: origin + valid ends
         if (r != RAY_INVALID) {
-            int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-            bx0 = min(bx0, x1); by0 = min(by0, y1); bx1 = max(bx1, x1); by1 = max(by1, y1);
-            int adx = abs(x1 - x0), ady = abs(y1 - y0);
+            const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+            gx0 = min(gx0, x1); gy0 = min(gy0, y1); gx1 = max(gx1, x1); gy1 = max(gy1, y1);
+            const int adx = abs(x1 - x0), ady = abs(y1 - y0);
             L += (unsigned long long)(max(adx, ady) + 1);
             R += 1;
         }
+        bx0 = min(bx0, gx0); by0 = min(by0, gy0); bx1 = max(bx1, gx1); by1 = max(by1, gy1);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            gx0 = min(gx0, __shfl_xor(gx0, off, 64));
+            gy0 = min(gy0, __shfl_xor(gy0, off, 64));
+            gx1 = max(gx1, __shfl_xor(gx1, off, 64));
+            gy1 = max(gy1, __shfl_xor(gy1, off, 64));
+        }
+        if ((tid & 63) == 0) gbox[b0 >> 6] = make_int4(gx0, gy0, gx1, gy1);
     }
     if (R) {
         atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
@@ -970,7 +1034,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         L += __shfl_xor(L, off, 64);
         R += __shfl_xor(R, off, 64);
     }
-    if ((tid & 63) == 0 && R) {
+    if ((tid & 63) == 0 && R && part == 0) {
         atomicAdd(&state[s].step_cells, L);
         atomicAdd(&state[s].tot_cells, L);
         atomicAdd(&state[s].tot_rays, R);
@@ -983,99 +1047,109 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     const float lf = geom.lf, lo = geom.lo;
     unsigned touched = 0;
 
-    for (int ty = ty0; ty <= ty1; ++ty) {
-        for (int tx = tx0; tx <= tx1; ++tx) {
-            const int X0 = tx * TILE, Y0 = ty * TILE_H;
-            const int X1 = X0 + TILE, Y1 = Y0 + TILE_H;
-            for (int k = tid; k < 2 * TILE_CELLS / 4; k += UPD_THREADS)
-                reinterpret_cast<uint4 *>(smem)[k] = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
-            __syncthreads();
-            bool any = false;
-            for (int b = tid; b < n; b += UPD_THREADS) {
-                unsigned r = rays[b];
-                if (r == RAY_INVALID) continue;
-                int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-                if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
-                if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {
-                    atomicMin(&first_hit[(y1 - Y0) * TILE + (x1 - X0)], (unsigned)b);  // bresenhamCellOcc (:266)
-                    any = true;
-                }
-                RayWalk w = ray_walk(x0, y0, x1, y1);
-                int lo_i, hi_i;
-                bool in = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i) : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
-                if (!in) continue;
-                if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
-                if (lo_i > hi_i) continue;
+    const int ntx = tx1 - tx0 + 1, ntiles = ntx * (ty1 - ty0 + 1);
+    for (int t = part; t < ntiles; t += parts) {
+        const int ty = ty0 + t / ntx, tx = tx0 + t % ntx;
+        const int X0 = tx * TILE, Y0 = ty * TILE_H;
+        const int X1 = X0 + TILE, Y1 = Y0 + TILE_H;
+        for (int k = tid; k < 2 * UPD_TILE_WORDS / 4; k += UPD_THREADS)
+            reinterpret_cast<uint4 *>(smem)[k] = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
+        __syncthreads();
+        bool any = false;
+        for (int b0 = tid & ~63; b0 < n; b0 += UPD_THREADS) {
+            // wave-uniform fan-group test (scalar)
+            const int4 gb = gbox[b0 >> 6];
+            const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
+            const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
+            if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
+            const int b = b0 + (tid & 63);
+            if (b >= n) continue;
+            const unsigned r = rays[b];
+            if (r == RAY_INVALID) continue;
+            const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+            if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
+            if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {
+                atomicMin(&first_hit[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], (unsigned)b);  // bresenhamCellOcc (:266)
                 any = true;
-                const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
-                const int q = (int)(num / (unsigned)w.da);
-                int err = (int)(num - (unsigned)q * (unsigned)w.da);
-                // local LDS index of step lo_i and its increments along the major / minor axis
-                const int la = w.x_major ? 1 : TILE;
-                const int lb = w.x_major ? TILE : 1;
-                const int ax = w.a0 + w.sa * lo_i - (w.x_major ? X0 : Y0);
-                const int bx = w.b0 + w.sb * q - (w.x_major ? Y0 : X0);
-                int li = ax * la + bx * lb;
-                const int da_step = w.sa * la, db_step = w.sb * lb;
-                for (int i = lo_i; i <= hi_i; ++i) {
-                    atomicMin(&first_free[li], (unsigned)b);  // bresenhamCellFree (:302-312)
-                    li += da_step;
-                    err += w.db;
-                    if (err >= w.da) {
-                        err -= w.da;
-                        li += db_step;
-                    }
+            }
+            RayWalk w = ray_walk(x0, y0, x1, y1);
+            int lo_i, hi_i;
+            bool in = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i) : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
+            if (!in) continue;
+            if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
+            if (lo_i > hi_i) continue;
+            any = true;
+            const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
+            const int q = (int)(num / (unsigned)w.da);
+            int err = (int)(num - (unsigned)q * (unsigned)w.da);
+            // local LDS index of step lo_i and its increments along the major / minor axis
+            const int la = w.x_major ? 1 : UPD_STRIDE;
+            const int lb = w.x_major ? UPD_STRIDE : 1;
+            const int ax = w.a0 + w.sa * lo_i - (w.x_major ? X0 : Y0);
+            const int bx = w.b0 + w.sb * q - (w.x_major ? Y0 : X0);
+            int li = ax * la + bx * lb;
+            const int da_step = w.sa * la, db_step = w.sb * lb;
+            for (int i = lo_i; i <= hi_i; ++i) {
+                atomicMin(&first_free[li], (unsigned)b);  // bresenhamCellFree (:302-312)
+                li += da_step;
+                err += w.db;
+                if (err >= w.da) {
+                    err -= w.da;
+                    li += db_step;
                 }
             }
-            if (!__syncthreads_or(any)) continue;
-            // apply: wave w handles rows w, w+4, ...; lane = column -> 512 B coalesced rows;
-            // the loads of a batch of rows are issued before any store of that batch.
-            const int col = tid & 63;
-            const int gx = X0 + col;
-            float *tl = lvw + (size_t)(tx + ty * g.tiles_x) * TILE_BLOCK_WORDS;
-            int *tu = reinterpret_cast<int *>(tl + TILE_CELLS);
-            constexpr int RPW = TILE_H / (UPD_THREADS / 64);  // rows per wave
-            constexpr int NB = S2D_APPLY_BATCH < RPW ? S2D_APPLY_BATCH : RPW;
-#pragma unroll
-            for (int k0 = 0; k0 < RPW; k0 += NB) {
-                unsigned fh[NB], ff[NB];
-                float cv[NB];
-#pragma unroll
-                for (int k = 0; k < NB; ++k) {
-                    const int row = (tid >> 6) + (k0 + k) * (UPD_THREADS / 64);
-                    const int gy = Y0 + row;
-                    unsigned h = first_hit[row * TILE + col];
-                    unsigned f = first_free[row * TILE + col];
-                    if (gx >= g.sx || gy >= g.sy) h = f = W_NONE;
-                    fh[k] = h;
-                    ff[k] = f;
-                    if ((h & f) != W_NONE) cv[k] = tl[row * TILE + col];
-                }
-#pragma unroll
-                for (int k = 0; k < NB; ++k) {
-                    const unsigned h = fh[k], f = ff[k];
-                    if ((h & f) == W_NONE) continue;
-                    const int row = (tid >> 6) + (k0 + k) * (UPD_THREADS / 64);
-                    float l = cv[k];
-                    int upd;
-                    if (h == W_NONE) {
-                        l = l + lf;        // updateSetFree (GridMapLogOdds.h:120-124)
-                        upd = mark_free;
-                    } else {
-                        if (f < h) {
-                            l = l + lf;    // bresenhamCellFree by an earlier beam
-                            l = l - lf;    // updateUnsetFree (GridMapLogOdds.h:126-129)
-                        }
-                        if (l < 50.0f) l = l + lo;  // updateSetOccupied (:108-114)
-                        upd = mark_occ;
-                    }
-                    tl[row * TILE + col] = l;
-                    tu[row * TILE + col] = upd;
-                    ++touched;
-                }
-            }
-            __syncthreads();
         }
+        if (!__syncthreads_or(any)) continue;
+        // apply: thread owns quads q = tid + j * 256 (16 quads per 64-cell row): 16-B LDS reads,
+        // 16-B global loads / stores of both planes for every quad holding a mark.  Cells outside
+        // the map (padding of edge tiles) never carry marks and are rewritten unchanged.
+        float *tl = lvw + (size_t)(tx + ty * g.tiles_x) * TILE_BLOCK_WORDS;
+        int *tu = reinterpret_cast<int *>(tl + TILE_CELLS);
+        uint4 qh[UPD_QUADS], qf[UPD_QUADS];
+        float4 ql[UPD_QUADS];
+        int4 qu[UPD_QUADS];
+        bool qm[UPD_QUADS];
+#pragma unroll
+        for (int j = 0; j < UPD_QUADS; ++j) {
+            const int qi = tid + j * UPD_THREADS;
+            const int row = qi >> 4, c4 = (qi & 15) << 2;
+            qh[j] = *reinterpret_cast<const uint4 *>(&first_hit[row * UPD_STRIDE + c4]);
+            qf[j] = *reinterpret_cast<const uint4 *>(&first_free[row * UPD_STRIDE + c4]);
+            qm[j] = quad_marked(qh[j], qf[j]);
+            if (qm[j]) {
+                ql[j] = *reinterpret_cast<const float4 *>(&tl[row * TILE + c4]);
+#if S2D_APPLY_UPD_LOAD
+                qu[j] = *reinterpret_cast<const int4 *>(&tu[row * TILE + c4]);
+#endif
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UPD_QUADS; ++j) {
+            if (!qm[j]) continue;
+            const int qi = tid + j * UPD_THREADS;
+            const int row = qi >> 4, c4 = (qi & 15) << 2;
+#if S2D_APPLY_UPD_LOAD
+            touched += apply_cell(ql[j].x, qu[j].x, qh[j].x, qf[j].x, lf, lo, mark_free, mark_occ);
+            touched += apply_cell(ql[j].y, qu[j].y, qh[j].y, qf[j].y, lf, lo, mark_free, mark_occ);
+            touched += apply_cell(ql[j].z, qu[j].z, qh[j].z, qf[j].z, lf, lo, mark_free, mark_occ);
+            touched += apply_cell(ql[j].w, qu[j].w, qh[j].w, qf[j].w, lf, lo, mark_free, mark_occ);
+            *reinterpret_cast<float4 *>(&tl[row * TILE + c4]) = ql[j];
+            *reinterpret_cast<int4 *>(&tu[row * TILE + c4]) = qu[j];
+#else
+            int u[4];
+            const int t0 = apply_cell(ql[j].x, u[0], qh[j].x, qf[j].x, lf, lo, mark_free, mark_occ);
+            const int t1 = apply_cell(ql[j].y, u[1], qh[j].y, qf[j].y, lf, lo, mark_free, mark_occ);
+            const int t2 = apply_cell(ql[j].z, u[2], qh[j].z, qf[j].z, lf, lo, mark_free, mark_occ);
+            const int t3 = apply_cell(ql[j].w, u[3], qh[j].w, qf[j].w, lf, lo, mark_free, mark_occ);
+            touched += t0 + t1 + t2 + t3;
+            *reinterpret_cast<float4 *>(&tl[row * TILE + c4]) = ql[j];
+            if (t0) tu[row * TILE + c4 + 0] = u[0];
+            if (t1) tu[row * TILE + c4 + 1] = u[1];
+            if (t2) tu[row * TILE + c4 + 2] = u[2];
+            if (t3) tu[row * TILE + c4 + 3] = u[3];
+#endif
+        }
+        __syncthreads();
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);

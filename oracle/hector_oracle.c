@@ -87,6 +87,13 @@ static inline float ho_sinf(const ho_ctx *c, float x) { return c->use_libm ? sin
 static inline float ho_cosf(const ho_ctx *c, float x) { return c->use_libm ? cosf(x) : odm_cosf(x); }
 static inline float ho_expf(const ho_ctx *c, float x) { return c->use_libm ? (float)exp((double)x) : odm_expf(x); }
 
+/* (int)v of OccGridMapBase.h:135/:154 for v in int range; NaN or out-of-range (undefined behaviour in
+ * the reference, INT_MIN on x86) -> -1, which the bounds check of :226-238 cancels like INT_MIN */
+static inline int ho_cell_of(float v)
+{
+    return (v > -2147483648.0f && v < 2147483648.0f) ? (int)v : -1;
+}
+
 /* GridMapLogOddsFunctions::probToLogOdds  H/map/GridMapLogOdds.h:153-157 */
 static float ho_prob_to_logodds(float prob)
 {
@@ -268,7 +275,9 @@ void ho_get_trace(const ho_ctx *c, float *out) { memcpy(out, c->trace, sizeof(fl
 static inline void ho_interp(const ho_ctx *c, const ho_level *L, float x, float y, float *v, float *gx, float *gy)
 {
     /* pointOutOfMapBounds  MapDimensionProperties.h:61-64 */
-    if ((x < 0.0f) || (x > L->lim[0]) || (y < 0.0f) || (y > L->lim[1])) {
+    /* NaN-safe form of the same test: a NaN coordinate (diverged pose) counts as out of map, where the
+     * reference would index the grid with (int)NaN (undefined behaviour) */
+    if (!(x >= 0.0f) || !(x <= L->lim[0]) || !(y >= 0.0f) || !(y <= L->lim[1])) {
         *v = 0.0f; *gx = 0.0f; *gy = 0.0f;
         return;
     }
@@ -534,14 +543,14 @@ static void ho_update_level(ho_ctx *c, int lvl, const float *xy, int n, float ox
     float ox_l = ox * f, oy_l = oy * f;
     float bx = mp[0] + (cs * ox_l + nsn * oy_l);
     float by = mp[1] + (sn * ox_l + cs * oy_l);
-    int bxi = (int)(bx + 0.5f), byi = (int)(by + 0.5f);
+    int bxi = ho_cell_of(bx + 0.5f), byi = ho_cell_of(by + 0.5f);
     for (int i = 0; i < n; ++i) {
         float px = xy[2 * i] * f, py = xy[2 * i + 1] * f;
         float ex = mp[0] + (cs * px + nsn * py);
         float ey = mp[1] + (sn * px + cs * py);
         ex += 0.5f;
         ey += 0.5f;
-        int exi = (int)ex, eyi = (int)ey;
+        int exi = ho_cell_of(ex), eyi = ho_cell_of(ey);
         if (bxi != exi || byi != eyi) ho_update_line(c, L, bxi, byi, exi, eyi, mf, mo);
     }
     L->last_update_index++;          /* setUpdated  GridMapBase.h:333 */

@@ -6,7 +6,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "creating-2d-laser-slam-from-scratch_amd")
-for p in (os.path.join(PKG, "python"), os.path.join(REPO, "oracle")):
+for p in (os.path.join(PKG, "python"), os.path.join(REPO, "oracle"), REPO):
     if p not in sys.path:
         sys.path.insert(0, p)
 

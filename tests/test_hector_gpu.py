@@ -8,6 +8,8 @@ Bar (BASELINE.json north_star):
   * pose within POSE_TOL_M / POSE_TOL_RAD of the oracle in the reference's sequential order
     (the Hessian sums are reassociated by the parallel reduction).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -261,3 +263,94 @@ def test_batched_device_ragged(gpu):
             ol, ou = oras[s].level(lvl)
             np.testing.assert_array_equal(m["upd"], ou, err_msg=f"s={s} lvl={lvl}")
             np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol), err_msg=f"s={s} lvl={lvl}")
+
+
+# ----------------------------------------------------------------------------- golden fixtures on the GPU
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("name", sorted(f for f in os.listdir(GOLD) if f.startswith("hector_")))
+def test_golden_fixture(gpu, name):
+    """Committed oracle fixtures (tests/golden, oracle/make_golden.py) replayed through the C-ABI.
+    Fixtures in the GPU reduction order (reduce_threads 256) must match bit for bit (NaN == NaN for the
+    diverging case); the sequential-order fixture within the north-star pose tolerance."""
+    d = np.load(os.path.join(GOLD, name))
+    levels, size = int(d["levels"]), int(d["size"])
+    fleet = HectorFleet(1, 0.05, size, (0.5, 0.5), levels, max_points=1081)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(*[float(v) for v in d["thresholds"]])
+    exact = int(d["reduce_threads"]) == T_RED
+    for k in range(len(d["counts"])):
+        gp, gc, gd = fleet.update(0, d["points"][k, : d["counts"][k]])
+        if exact:
+            assert gd == bool(d["did_update"][k]), k
+            np.testing.assert_array_equal(gp, d["poses"][k], err_msg=f"scan {k}")
+            np.testing.assert_array_equal(gc, d["covs"][k], err_msg=f"scan {k}")
+            if gd:
+                assert fleet.poses()[3][0] == int(d["sum_L"][k]), k
+        else:
+            e = np.abs(gp.astype(np.float64) - d["poses"][k].astype(np.float64))
+            assert e[0] <= POSE_TOL_M and e[1] <= POSE_TOL_M and e[2] <= POSE_TOL_RAD, (k, e)
+    if exact:
+        for lvl in range(levels):
+            m = fleet.get_map(0, lvl)
+            idx = np.nonzero(m["upd"].ravel() >= 0)[0]
+            np.testing.assert_array_equal(idx, d[f"l{lvl}_idx"])
+            np.testing.assert_array_equal(_bits(m["logodds"].ravel()[idx]), d[f"l{lvl}_logodds_bits"])
+            np.testing.assert_array_equal(m["upd"].ravel()[idx], d[f"l{lvl}_upd"])
+            np.testing.assert_array_equal(m["occ"].ravel()[idx], d[f"l{lvl}_publish"])
+            assert m["update_index"] == int(d[f"l{lvl}_update_index"])
+
+
+def _pair_small(size=64, levels=1):
+    fleet = HectorFleet(1, 0.05, size, (0.5, 0.5), levels, max_points=64)
+    ora = O.HectorOracle(0.05, size, (0.5, 0.5), levels, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+    return fleet, ora
+
+
+def _same_level(fleet, ora, lvl=0):
+    m = fleet.get_map(0, lvl)
+    ol, ou = ora.level(lvl)
+    np.testing.assert_array_equal(m["upd"], ou)
+    np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))
+
+
+def test_once_per_scan_hand_built(gpu):
+    """The hand-derived once-per-scan sequences of tests/test_oracle_cpu.py on the GPU."""
+    fleet, ora = _pair_small()
+    pose = np.zeros(3, np.float32)
+    for pts in (np.array([[10.0, 0.0]], np.float32),
+                np.array([[10.0, 0.0], [5.0, 0.0], [13.0, 0.0], [12.0, 0.0], [8.0, 0.0], [10.0, 0.0]], np.float32)):
+        fleet.update_by_scan(0, pts, pose)
+        ora.update_by_scan(pts, pose)
+        _same_level(fleet, ora)
+
+
+def test_occupied_clamp_at_50(gpu):
+    fleet, ora = _pair_small()
+    l, u = ora.level(0)
+    l = l.copy()
+    l[32, 40], l[32, 41], l[32, 36] = 49.9, 50.0, 1e30
+    ora.set_level(0, l, u)
+    fleet.set_map(0, 0, l, u)
+    pose = np.zeros(3, np.float32)
+    for pts in (np.array([[8.0, 0.0]], np.float32), np.array([[9.0, 0.0], [4.0, 0.0]], np.float32)):
+        fleet.update_by_scan(0, pts, pose)
+        ora.update_by_scan(pts, pose)
+        _same_level(fleet, ora)
+
+
+def test_nan_pose_is_out_of_map(gpu):
+    """A diverged pose must not write any cell (GPU float->int would otherwise map NaN to cell 0)."""
+    fleet, ora = _pair_small(128, 2)
+    pts = np.array([[10.0, 0.0], [0.0, 7.0], [-3.0, -3.0]], np.float32)
+    for pose in (np.array([np.nan, 0.0, 0.0], np.float32), np.array([0.0, 0.0, np.nan], np.float32)):
+        fleet.update_by_scan(0, pts, pose)
+        ora.update_by_scan(pts, pose)
+    for lvl in range(2):
+        _same_level(fleet, ora, lvl)
+        assert (fleet.get_map(0, lvl)["upd"] >= 0).sum() == 0
+    gp, _ = fleet.match(0, pts, np.array([np.nan] * 3, np.float32))
+    assert np.isnan(gp).all()

@@ -1,0 +1,144 @@
+"""Host logic on the CPU: the DataContainer mirror, the synthetic scan generator, bench.py's
+accounting helpers, and bench's rank aggregation over torch.distributed (gloo, world_size 2)."""
+import json
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import bench
+from slam2d import synth
+from slam2d.hector import DataContainer
+
+
+# ----------------------------------------------------------------------------- DataContainer
+def test_datacontainer_setfrom_scales_points_and_origo():
+    """DataPointContainer::setFrom (scan/DataPointContainer.h:46-58): points and origo * factor."""
+    d = DataContainer()
+    d.add([2.0, 4.0])
+    d.add([-1.0, 0.5])
+    d.setOrigo([3.0, -2.0])
+    e = DataContainer()
+    e.setFrom(d, 0.5)
+    assert e.getSize() == 2
+    np.testing.assert_array_equal(e.getVecEntry(0), np.float32([1.0, 2.0]))
+    np.testing.assert_array_equal(e.getOrigo(), np.float32([1.5, -1.0]))
+    e.clear()
+    assert e.getSize() == 0
+
+
+def test_datacontainer_from_points_roundtrip():
+    pts = np.random.default_rng(0).normal(size=(17, 2)).astype(np.float32)
+    d = DataContainer.from_points(pts, (0.25, 0.5))
+    np.testing.assert_array_equal(d.points(), pts)
+    d.add([9.0, 9.0])
+    assert d.getSize() == 18 and d.getVecEntry(17)[0] == 9.0
+
+
+# ----------------------------------------------------------------------------- synthetic scans
+def test_synth_deterministic_and_filtered():
+    a = synth.make_streams(2, 6, seed=5)
+    b = synth.make_streams(2, 6, seed=5)
+    np.testing.assert_array_equal(a.points, b.points)
+    np.testing.assert_array_equal(a.counts, b.counts)
+    assert a.points.shape == (2, 6, synth.N_BEAMS, 2)
+    assert (a.counts > 900).all() and (a.counts <= synth.N_BEAMS).all()
+    # hector_slam.cc:336-353 filters: 0.2 m < d < 20 m (points are in map scale x20)
+    for s in range(2):
+        for k in range(6):
+            p = a.points[s, k, : a.counts[s, k]] / 20.0
+            d = np.hypot(p[:, 0], p[:, 1])
+            assert d.min() > 0.2 and d.max() < 20.0
+
+
+def test_synth_trajectory_step_bounds():
+    """<= 0.1 m and <= 5 deg per scan."""
+    S = synth.make_streams(3, 50, seed=9)
+    for s in range(3):
+        g = S.gt[s]
+        step = np.hypot(np.diff(g[:, 0]), np.diff(g[:, 1]))
+        dth = np.abs(np.angle(np.exp(1j * np.diff(g[:, 2]))))
+        assert step.max() <= 0.1 + 1e-9 and dth.max() <= math.radians(5) + 1e-9
+
+
+def test_synth_beam_geometry():
+    a = synth.beam_angles()
+    assert len(a) == 1081
+    assert np.isclose(a[0], -3 * math.pi / 4, atol=1e-6)
+    assert np.allclose(np.diff(a), math.radians(0.25), atol=1e-6)
+
+
+# ----------------------------------------------------------------------------- bench accounting
+def test_algorithmic_bytes_formula():
+    """B_match = gn_points x 24 B, B_update = ΣL x 16 B, read-only = B_match + ΣL x 8."""
+    ctr = {"gn_points": 1000, "cells": 5000, "rays": 70}
+    ab = bench.algorithmic_bytes(ctr, 3)
+    assert ab["match"] == 24000 and ab["update"] == 80000 and ab["total"] == 104000
+    assert ab["read_only"] == 24000 + 40000 and ab["bin"] == 70 * 12
+
+
+def test_kernel_symbol():
+    kt = {"match": (1.0, 3), "bin": (0.0, 0), "update": (2.0, 3)}
+    assert bench.kernel_symbol("update", kt) == "hs_update_kernel"
+    kt["bin"] = (0.5, 3)
+    assert bench.kernel_symbol("update", kt) == "hs_tile_kernel"
+    assert bench.kernel_symbol("match", kt) == "hs_match_kernel"
+
+
+def test_pmc_traffic_lookup(tmp_path, monkeypatch):
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"entries": [{"kernel": "hs_update_kernel", "config": "northstar", "streams": 1024,
+                                          "traffic_bytes_per_launch": 123, "source": "x"}]}))
+    monkeypatch.setattr(bench, "PMC_SUMMARY", str(p))
+    assert bench.pmc_traffic("hs_update_kernel", "northstar", 1024)["traffic_bytes_per_launch"] == 123
+    assert bench.pmc_traffic("hs_update_kernel", "c2", 1024) is None
+
+
+def test_committed_pmc_summary_is_consistent():
+    """profiles/pmc_traffic.json: every entry points at a committed summary file."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(repo, "profiles", "pmc_traffic.json")) as f:
+        d = json.load(f)
+    for e in d["entries"]:
+        assert os.path.exists(os.path.join(repo, e["source"])), e["source"]
+        assert e["traffic_bytes_per_launch"] == int((2 * e["fetch_kb"] + e["write_kb"]) * 1024)
+
+
+# ----------------------------------------------------------------------------- distributed (gloo)
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _agg_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t, u = bench.aggregate_over_ranks(1.0 + rank, 100.0 * (rank + 1), torch.device("cpu"))
+    out[rank] = (t, u)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_aggregation_gloo_world2():
+    """bench.py: value = units of ALL ranks / the SLOWEST rank's time (barrier + max over ranks)."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_agg_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    for r in range(world):
+        assert res[r] == (2.0, 300.0)
+
+
+def test_rank_aggregation_single_process():
+    import torch
+
+    assert bench.aggregate_over_ranks(0.5, 7.0, torch.device("cpu")) == (0.5, 7.0)

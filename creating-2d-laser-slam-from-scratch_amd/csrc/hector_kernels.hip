@@ -24,6 +24,10 @@
 #include "detmath.h"
 #include "hector_internal.h"
 
+#ifndef S2D_MATCH_ABL
+#define S2D_MATCH_ABL 0  // diagnostic builds only: 1 hardware exp, 2 no cell gathers
+#endif
+
 namespace s2d {
 
 // ---------------------------------------------------------------------------------------- helpers
@@ -68,7 +72,11 @@ __device__ __forceinline__ bool pose_diff_larger(const float *p1, const float *p
 // GridMapLogOddsFunctions::getGridProbability  H/map/GridMapLogOdds.h:136-140
 __device__ __forceinline__ float cell_prob(float l)
 {
+#if S2D_MATCH_ABL == 1
+    float odds = __expf(l);  // diagnostic only
+#else
     float odds = sdm_expf(l);
+#endif
     return __fdiv_rn(odds, odds + 1.0f);
 }
 
@@ -99,28 +107,55 @@ __device__ __forceinline__ void solve3(const float *m, const float *b, float *d)
 
 // --------------------------------------------------------------------------------- k1: match
 // Per point: OccGridMapUtil::getCompleteHessianDerivs body (H/map/OccGridMapUtil.h:94-126) with
-// interpMapValueWithDerivatives (:139-228).  Accumulates into acc[9] =
-// {dTr0, dTr1, dTr2, H00, H11, H22, H01, H02, H12}.
-__device__ __forceinline__ void point_terms(const float *__restrict__ lvl_words, const LevelGeom &g, float tx,
-                                            float ty, float cs, float sn, float px, float py, float *acc)
+// interpMapValueWithDerivatives (:139-228), split in two phases so that a thread's gathers for a
+// batch of points are all in flight before the first one is consumed:
+//   point_fetch: transform, bounds test, the 4 neighbour log-odds (raw);
+//   point_accum: probabilities, bilinear value + corrected gradients, accumulate into acc[9] =
+//                {dTr0, dTr1, dTr2, H00, H11, H22, H01, H02, H12}.
+struct PointFetch {
+    float px, py, fx, fy;
+    float l[4];
+    bool in;
+};
+
+__device__ __forceinline__ void point_fetch(const float *__restrict__ lvl_words, const LevelGeom &g, float tx,
+                                            float ty, float cs, float sn, float px, float py, PointFetch &pf)
 {
     float nsn = -sn;
     float x = tx + (cs * px + nsn * py);
     float y = ty + (sn * px + cs * py);
+    pf.px = px;
+    pf.py = py;
+    pf.in = (x >= 0.0f) && (x <= g.lim[0]) && (y >= 0.0f) && (y <= g.lim[1]);  // NaN -> out of map
+    if (pf.in) {
+        int ix = (int)x, iy = (int)y;
+        pf.fx = x - (float)ix;
+        pf.fy = y - (float)iy;
+        // 4 neighbours (:160-192); ix <= sx-2, iy <= sy-2 by the bounds check
+#if S2D_MATCH_ABL == 2
+        pf.l[0] = (float)(ix & 7) * 0.01f; pf.l[1] = (float)(iy & 7) * 0.01f; pf.l[2] = 0.0f; pf.l[3] = 0.0f;
+#else
+        pf.l[0] = lvl_words[cell_word(g, ix, iy)];
+        pf.l[1] = lvl_words[cell_word(g, ix + 1, iy)];
+        pf.l[2] = lvl_words[cell_word(g, ix, iy + 1)];
+        pf.l[3] = lvl_words[cell_word(g, ix + 1, iy + 1)];
+#endif
+    }
+}
+
+__device__ __forceinline__ void point_accum(const PointFetch &pf, float cs, float sn, float *acc)
+{
     float v, gx, gy;
-    if (!(x >= 0.0f) || !(x <= g.lim[0]) || !(y >= 0.0f) || !(y <= g.lim[1])) {  // NaN -> out of map
+    if (!pf.in) {
         v = 0.0f;
         gx = 0.0f;
         gy = 0.0f;
     } else {
-        int ix = (int)x, iy = (int)y;
-        float fx = x - (float)ix;
-        float fy = y - (float)iy;
-        // 4 neighbours (:160-192); ix <= sx-2, iy <= sy-2 by the bounds check
-        float i0 = cell_prob(lvl_words[cell_word(g, ix, iy)]);
-        float i1 = cell_prob(lvl_words[cell_word(g, ix + 1, iy)]);
-        float i2 = cell_prob(lvl_words[cell_word(g, ix, iy + 1)]);
-        float i3 = cell_prob(lvl_words[cell_word(g, ix + 1, iy + 1)]);
+        const float fx = pf.fx, fy = pf.fy;
+        float i0 = cell_prob(pf.l[0]);
+        float i1 = cell_prob(pf.l[1]);
+        float i2 = cell_prob(pf.l[2]);
+        float i3 = cell_prob(pf.l[3]);
         float dx1 = i0 - i1;
         float dx2 = i2 - i3;
         float dy1 = i0 - i2;
@@ -131,6 +166,7 @@ __device__ __forceinline__ void point_terms(const float *__restrict__ lvl_words,
         gx = -((dx1 * yfi) + (dx2 * fy));
         gy = -((dy1 * xfi) + (dy2 * fx));
     }
+    const float px = pf.px, py = pf.py;
     float fun = 1.0f - v;
     // sinRot/cosRot (:87-88) are the same values as the transform's sn/cs
     float rot = ((-sn * px - cs * py) * gx + (cs * px - sn * py) * gy);
@@ -145,6 +181,11 @@ __device__ __forceinline__ void point_terms(const float *__restrict__ lvl_words,
     acc[8] = acc[8] + gy * rot;
 }
 
+#ifndef S2D_MATCH_BATCH
+#define S2D_MATCH_BATCH 2
+#endif
+constexpr int MATCH_BATCH = S2D_MATCH_BATCH;  // points per thread with gathers in flight together
+
 // One Gauss-Newton step, ScanMatcher::estimateTransformationLogLh (H/matcher/ScanMatcher.h:107-139).
 // Every thread ends with the same H, b and estimate (xor-butterfly reductions are symmetric).
 __device__ __forceinline__ void gn_step(const float *__restrict__ cells, const LevelGeom &g,
@@ -157,9 +198,20 @@ __device__ __forceinline__ void gn_step(const float *__restrict__ cells, const L
     float acc[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
-    for (int i = tid; i < n; i += MATCH_THREADS) {
-        float2 p = pts[i];
-        point_terms(cells, g, est[0], est[1], cs, sn, p.x * f, p.y * f, acc);
+    // per-thread order of the points is i = tid, tid + 256, ... (the oracle's reduce_threads order)
+    for (int i0 = tid; i0 < n; i0 += MATCH_THREADS * MATCH_BATCH) {
+        PointFetch pf[MATCH_BATCH];
+#pragma unroll
+        for (int j = 0; j < MATCH_BATCH; ++j) {
+            const int i = i0 + j * MATCH_THREADS;
+            if (i < n) {
+                const float2 p = pts[i];
+                point_fetch(cells, g, est[0], est[1], cs, sn, p.x * f, p.y * f, pf[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < MATCH_BATCH; ++j)
+            if (i0 + j * MATCH_THREADS < n) point_accum(pf[j], cs, sn, acc);
     }
     // 64-lane xor butterfly, offsets 32..1
 #pragma unroll

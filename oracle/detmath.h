@@ -140,6 +140,35 @@ static inline double odm_exp(double x)
 /* float-in / float-out wrappers: the single rounding point */
 static inline float odm_sinf(float x) { return (float)odm_sin((double)x); }
 static inline float odm_cosf(float x) { return (float)odm_cos((double)x); }
-static inline float odm_expf(float x) { return (float)odm_exp((double)x); }
+/* exp for float arguments in IEEE float: the same op sequence as csrc/detmath.h sdm_expf
+ * (Cody-Waite by ln2 with a 16-bit hi part, degree-7 Taylor, exact 2^k scaling; <= 1 ulp). */
+static inline float odm_pow2i(int k) /* 2^k, k in [-126, 127] */
+{
+    union { unsigned int u; float f; } v;
+    v.u = (unsigned int)(k + 127) << 23;
+    return v.f;
+}
+static inline float odm_expf(float x)
+{
+    /* branch-free (selects only, so the GPU keeps its gathers in flight); the value equals
+     * x != x ? x : x > 88.72284 ? inf : x < -103.97909 ? 0 : p * 2^k (two-step scaling past 2^-126) */
+    const float xc = (x == x) ? ((x > 88.72284f) ? 88.72284f : ((x < -103.97909f) ? -103.97909f : x)) : 0.0f;
+    const float k = floorf(xc * 1.44269502f + 0.5f);
+    float r = xc - k * 0.693145751953125f;
+    r = r - k * 1.42860677e-06f;
+    float p = 1.98412701e-04f;
+    p = 1.38888892e-03f + r * p;
+    p = 8.33333377e-03f + r * p;
+    p = 4.16666679e-02f + r * p;
+    p = 1.66666672e-01f + r * p;
+    p = 0.5f + r * p;
+    p = 1.0f + r * p;
+    p = 1.0f + r * p;
+    const int ki = (int)k;  /* in [-150, 128] */
+    const int k1 = ki > 127 ? 127 : (ki < -126 ? ki + 64 : ki);
+    const float m2 = ki > 127 ? 2.0f : (ki < -126 ? 5.42101086e-20f /* 2^-64 */ : 1.0f);
+    const float res = (p * odm_pow2i(k1)) * m2;
+    return (x != x) ? x : ((x > 88.72284f) ? HUGE_VALF : ((x < -103.97909f) ? 0.0f : res));
+}
 
 #endif

@@ -37,7 +37,7 @@ CONFIGS = {
     # BASELINE configs[1]: single-res 1024^2
     "c2": dict(map_size=1024, levels=1, streams=1024),
     # BASELINE configs[2]: 3-level 4096^2
-    "c3": dict(map_size=4096, levels=3, streams=256),
+    "c3": dict(map_size=4096, levels=3, streams=1024),  # 1024 x 176 MB pyramids = 180 GB of HBM
 }
 KERNELS = ("match", "bin", "update")
 PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")  # written by tools/summarize_profile.py

@@ -181,13 +181,121 @@ def pose_check(cfg, S, gpu_poses):
             "vs_ground_truth_rmse_theta_rad": float(np.sqrt(np.mean(egt[:, 2] ** 2)))}
 
 
+GM_METRIC = "particle-scans/sec (1081-beam) GMapping ComputeMap, particles sharded over GPUs"
+
+
+def gmapping_cpu_baseline(seconds=10.0):
+    """The GMapping oracle (C restatement of ComputeMap, -O3, 1 core) on particle-scans of the same
+    workload: one scan per call, consecutive particles."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    from slam2d import synth
+
+    ang = synth.beam_angles().astype(np.float64)
+    gt = synth.trajectory(8, 0.0)
+    ranges = synth.cast_ranges(gt[:1], synth.world_segments())[0].astype(np.float32)
+    rng = np.random.default_rng(1)
+    done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < 2000:
+        x, y, th = gt[0] + rng.normal(0, [0.05, 0.05, 0.02])
+        O.gm_compute(ranges, np.cos(ang), np.sin(ang), (x, y, np.cos(th), np.sin(th)))
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "particle-scans/s", "cores": 1, "kind": "port",
+            "sample": f"{done} ComputeMap calls (1081 beams, 1600^2 fresh map each), oracle/gmapping_oracle.c -O3 "
+                      "single thread (dense 41 MB memset per call, as the reference allocates its active patches)"}
+
+
+def run_gmapping(args, world, rank, dev):
+    """Config 4: every step, each rank runs GMapping::ComputeMap of the step's scan for its shard of
+    the particles (poses = ground truth + N(0, [5 cm, 5 cm, 0.02 rad]), seed 777), scores them against
+    their previous maps, and normalises the weights of ALL particles with one all-reduce (RCCL)."""
+    import torch
+    import torch.distributed as dist
+
+    from slam2d import synth
+    from slam2d.gmapping import GMappingFleet, normalize_weights
+
+    P_total = args.particles
+    P = P_total // world + (1 if rank < P_total % world else 0)
+    K, W = args.steps, args.warmup
+    T = K + W
+    ang = synth.beam_angles().astype(np.float64)
+    gt = synth.trajectory(T, 0.0)
+    ranges = synth.cast_ranges(gt, synth.world_segments()).astype(np.float32)
+    rng = np.random.default_rng(777 + rank)
+    noise = rng.normal(0, [0.05, 0.05, 0.02], size=(P, 3))
+    d_poses = torch.from_numpy(np.stack([GMappingFleet.poses4(gt[t] + noise) for t in range(T)])).to(dev)
+    d_ranges = torch.from_numpy(ranges).to(dev)
+    d_scores = torch.zeros(P, dtype=torch.int32, device=dev)
+    fleet = GMappingFleet(P)
+    fleet.set_beams(ang)
+    hs = torch.cuda.current_stream(dev).cuda_stream
+    nb = ranges.shape[1]
+
+    def step(t):
+        fleet.compute_device(d_poses[t].data_ptr(), d_ranges[t].data_ptr(), nb, d_scores.data_ptr(), hip_stream=hs)
+        return normalize_weights(d_scores)
+
+    for t in range(W):
+        step(t)
+    torch.cuda.synchronize()
+    fleet.kernel_times(reset=True)
+    fleet.set_timing(not args.no_timing)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    neff = 0.0
+    for t in range(W, T):
+        _, neff = step(t)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    fleet.set_timing(False)
+    kms, kn = fleet.kernel_times(reset=True)
+    s, h, f = fleet.scores()
+    t_max, total = aggregate_over_ranks(elapsed, float(P * K), dev)
+    value = total / t_max
+    if rank == 0:
+        roof = None
+        if kn:
+            # SURVEY.md §8d: per particle-scan Σ(L_b - 1) x 8 B (visits RMW) + hits x 32 B (16-B cell RMW)
+            alg = float(f.sum()) * 8 + float(h.sum()) * 32   # last step of this rank's particles
+            avg_s = kms / 1e3 / kn
+            roof = {"bound": "hbm", "kernel": "gm_compute_kernel", "achieved": round(alg / avg_s / 1e9, 2),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / avg_s / 1e9 / HBM_PEAK_GBS, 5),
+                    "traffic": None, "avg_launch_ms": round(kms / kn, 5), "alg_bytes_per_launch": int(alg),
+                    "particles_per_launch": P, "free_updates_per_particle": round(float(f.mean()), 1)}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = gmapping_cpu_baseline()
+        out = {"metric": GM_METRIC, "value": round(value, 1), "unit": "particle-scans/s", "n_gpus": world, "steps": K,
+               "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+               "vs_baseline": None, "dtype": "int32+f64", "data": "synthetic",
+               "config": {"workload": f"make_gmapping_map ComputeMap, 1600x1600 @0.05 m fresh map per scan, "
+                                      f"{P_total} particles x 1081 beams, weights all-reduced every step",
+                          "config": "gmapping", "particles": P_total, "particles_per_gpu": P,
+                          "parallelism": f"particles sharded x{world}"},
+               "roofline": roof, "cpu_baseline": cpu, "neff": neff}
+        if cpu:
+            out["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    fleet.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--streams", type=int, default=0, help="streams per GPU (0 = config default)")
-    ap.add_argument("--config", default="northstar", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="northstar", choices=sorted(CONFIGS) + ["gmapping"])
+    ap.add_argument("--particles", type=int, default=1024, help="gmapping: particles of the whole job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--no-copy-probe", action="store_true", help="skip the copy-bandwidth probe")
@@ -209,6 +317,8 @@ def main():
     from slam2d import synth
     from slam2d.hector import HectorFleet
 
+    if args.config == "gmapping":
+        return run_gmapping(args, world, rank, dev)
     cfg = dict(CONFIGS[args.config])
     B = args.streams or cfg["streams"]
     K, W = args.steps, args.warmup

@@ -1,0 +1,46 @@
+// gmapping_internal.h -- device data layout of the GMapping particle-map path (config 4).
+//
+// Reference: GMapping::ComputeMap (lesson4/src/gmapping/gmapping.cc:171-242) builds a FRESH
+// ScanMatcherMap per scan (:128-135) and counts, per cell, n (hits) and visits
+// (PointAccumulator, lesson4/include/lesson4/gmapping/grid/map.h:17-48).  The build evaluates it for
+// P candidate poses ("particles") of the same scan.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace s2d {
+
+constexpr int GM_TILE = 64;                 // tile width (cells)
+constexpr int GM_TILE_H = 32;               // tile height (cells)
+constexpr int GM_TILE_CELLS = GM_TILE * GM_TILE_H;
+// one tile = 4 planes of 2048 words: visits (int32), n (int32), acc.x (float), acc.y (float)
+constexpr int GM_TILE_BLOCK_WORDS = 4 * GM_TILE_CELLS;
+constexpr int GM_THREADS = 256;
+constexpr unsigned GM_RAY_INVALID = 0xFFFFFFFFu;
+constexpr unsigned GM_RAY_HIT = 0x80000000u;  // packed ray: hit flag | y << 16 | x
+
+// ScanMatcherMap geometry (G/grid/map.h:133-143, world2map :171-174) + ComputeMap parameters
+struct GmGeom {
+    int sx, sy;          // map size (multiple of the 32-cell patch, harray2d.h)
+    int sx2, sy2;        // map cell of the map centre
+    double cx, cy;       // map centre (world)
+    double delta;        // resolution
+    double max_range;    // maxRange: beams beyond are dropped (gmapping.cc:183)
+    double max_urange;   // maxUrange: beams beyond are clamped and not hits (:185-187, :209-214)
+    double occ_thresh;   // PublishMap occupancy threshold (gmapping.cc:150), used by the score
+    int tiles_x, tiles_y;
+    size_t particle_words;  // 4-byte words per particle map
+    int max_beams;
+    int pad_;
+};
+
+// Per-particle state: the tile box written by the last ComputeMap (cells outside it read as an
+// untouched fresh map: n = visits = 0, acc = 0) and the last step's counters.
+struct alignas(16) GmState {
+    int tx0, ty0, tx1, ty1;  // written tile box (tx1 < tx0: none)
+    int score;               // hits of this scan on occupied cells of the particle's previous map
+    int hits;                // hit beams (d < max_urange) of this scan
+    long long free_updates;  // Σ (num_points - 1): the free-cell visit updates of this scan
+};
+
+}  // namespace s2d

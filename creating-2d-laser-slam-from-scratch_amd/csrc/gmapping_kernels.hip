@@ -1,0 +1,330 @@
+// gmapping_kernels.hip -- MI355X kernels of the GMapping particle-map path (config 4).
+//
+//   gm_compute_kernel   one 256-thread workgroup per particle: GMapping::ComputeMap
+//                       (lesson4/src/gmapping/gmapping.cc:171-242) of the shared scan seen from the
+//                       particle's pose, into the particle's tiled (n, visits, acc) map, plus the
+//                       particle's score against its previous map (read before it is overwritten).
+//
+// Raster: GridLineTraversal::gridLine (lesson4/include/lesson4/gmapping/grid/gridlinetraversal.h:
+// 27-207) starts at the endpoint with the smaller major coordinate and, with decision variable
+// d = 2 db - da, steps the minor axis when d >= 0.  In closed form, step i from that start is
+//     (a_s + i, b_s + sb * q(i)),  q(i) = floor((2 db i + da) / (2 da)),  i in [0, da]
+// (checked against the incremental walk on 200k random lines), so every lane clips its line to
+// a tile directly.  points[0 .. num_points-2] (all but the end cell p1) get visits++ (:227-234);
+// the end cell of a hit beam gets n++, visits++ and acc += (float)hit (:236-240, map.h:37-48).
+// Counts are order-free integers (LDS atomicAdd on n << 16 | visits); acc is a float sum in beam
+// order, so a cell hit by several beams is summed sequentially by its first beam's lane.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "gmapping_internal.h"
+
+namespace s2d {
+
+constexpr int GM_STRIDE = 68;                          // LDS words per tile row (16-B rows)
+constexpr int GM_LDS_WORDS = GM_TILE_H * GM_STRIDE;    // one LDS tile array
+
+// Map::world2map (G/grid/map.h:171-174): round((p - center) / delta) + size/2, in double
+__device__ __forceinline__ void gm_world2map(const GmGeom &g, double wx, double wy, int &mx, int &my)
+{
+    mx = (int)round((wx - g.cx) / g.delta) + g.sx2;
+    my = (int)round((wy - g.cy) / g.delta) + g.sy2;
+}
+
+// packed ray: hit flag | (dy + 16384) << 16 | (dx + 16384), end cell relative to p0
+constexpr int GM_REL = 16384;
+__device__ __forceinline__ unsigned gm_pack(int dx, int dy, bool hit)
+{
+    return (hit ? GM_RAY_HIT : 0u) | ((unsigned)(dy + GM_REL) << 16) | (unsigned)(dx + GM_REL);
+}
+
+// One beam's grid line in (major a, minor b) coordinates, from its smaller-major end S.
+struct GmLine {
+    int as, bs, sb;   // start, minor direction
+    int da, db;       // |major|, |minor| extent
+    bool x_major;     // dy <= dx (gridlinetraversal.h:49)
+    int ilo, ihi;     // free step range (the step of p1 excluded)
+};
+
+__device__ __forceinline__ GmLine gm_line(int x0, int y0, int x1, int y1)
+{
+    GmLine l;
+    const int dx = abs(x1 - x0), dy = abs(y1 - y0);
+    l.x_major = dy <= dx;
+    int a0 = l.x_major ? x0 : y0, b0 = l.x_major ? y0 : x0;
+    int a1 = l.x_major ? x1 : y1, b1 = l.x_major ? y1 : x1;
+    const bool p1_is_start = a1 < a0;  // the walk starts at the smaller major coordinate
+    l.as = p1_is_start ? a1 : a0;
+    l.bs = p1_is_start ? b1 : b0;
+    const int be = p1_is_start ? b0 : b1;
+    l.sb = be > l.bs ? 1 : -1;
+    l.da = l.x_major ? dx : dy;
+    l.db = l.x_major ? dy : dx;
+    l.ilo = p1_is_start ? 1 : 0;                // p1 = step 0 or step da is not freed
+    l.ihi = p1_is_start ? l.da : l.da - 1;
+    return l;
+}
+
+// Steps of the line inside [A0, A1) x [B0, B1) (major x minor), intersected with [lo, hi].
+__device__ __forceinline__ bool gm_clip(const GmLine &l, int A0, int A1, int B0, int B1, int &lo, int &hi)
+{
+    lo = max(lo, A0 - l.as);
+    hi = min(hi, A1 - 1 - l.as);
+    if (lo > hi) return false;
+    // minor range as q = (b - bs) * sb
+    const int tlo = l.sb > 0 ? B0 - l.bs : l.bs - (B1 - 1);
+    const int thi = l.sb > 0 ? B1 - 1 - l.bs : l.bs - B0;
+    if (thi < 0) return false;
+    if (l.db == 0) return tlo <= 0;  // q == 0 everywhere
+    const unsigned two_da = 2u * (unsigned)l.da, two_db = 2u * (unsigned)l.db;
+    if (tlo > 0) {  // smallest i with q(i) >= tlo
+        const unsigned x = two_da * (unsigned)tlo - (unsigned)l.da;
+        lo = max(lo, (int)((x + two_db - 1u) / two_db));
+    }
+    {  // largest i with q(i) <= thi
+        const unsigned y = two_da * (unsigned)(thi + 1) - (unsigned)l.da;
+        hi = min(hi, (int)((y - 1u) / two_db));
+    }
+    return lo <= hi;
+}
+
+__global__ void __launch_bounds__(GM_THREADS)
+gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__restrict__ ranges, int n,
+                  const double *__restrict__ a_cos, const double *__restrict__ a_sin, int *__restrict__ maps,
+                  GmState *__restrict__ state, int *__restrict__ scores_out, int particle_begin)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned smem[];
+    unsigned *cnt = smem;                              // n << 16 | visits per cell of the tile
+    unsigned *first_hit = smem + GM_LDS_WORDS;         // lowest hitting beam per cell
+    unsigned *rays = smem + 2 * GM_LDS_WORDS;          // packed end cells
+    float2 *hitxy = reinterpret_cast<float2 *>(rays + ((n + 3) & ~3));   // (float)hit point
+    int4 *gbox = reinterpret_cast<int4 *>(hitxy + ((n + 1) & ~1));      // per 64-beam fan group
+    __shared__ int s_box[4];
+    __shared__ int s_red[GM_THREADS / 64][2];
+
+    const int p = particle_begin + blockIdx.x;
+    const int tid = threadIdx.x;
+    int *pm = maps + (size_t)p * g.particle_words;
+    GmState &st = state[p];
+    const double px = poses[4 * blockIdx.x], py = poses[4 * blockIdx.x + 1];
+    const double ct = poses[4 * blockIdx.x + 2], sn = poses[4 * blockIdx.x + 3];
+    int x0, y0;
+    gm_world2map(g, px, py, x0, y0);  // p0 = world2map(lp) (:176-179)
+    const int ptx0 = st.tx0, pty0 = st.ty0, ptx1 = st.tx1, pty1 = st.ty1;  // previous map's box
+
+    if (tid == 0) {
+        s_box[0] = g.sx; s_box[1] = g.sy; s_box[2] = -1; s_box[3] = -1;
+    }
+    __syncthreads();
+    // ---- rays (:185-214) + score against the previous map
+    int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
+    int score = 0, hits = 0;
+    for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
+        const int b = b0 + (tid & 63);
+        unsigned r = GM_RAY_INVALID;
+        int gx0 = x0, gy0 = y0, gx1 = x0, gy1 = y0;
+        if (b < n) {
+            double d = ranges[b];
+            if (!(d > g.max_range || d == 0.0 || !isfinite(d))) {
+                if (d > g.max_urange) d = g.max_urange;
+                const double ca = a_cos[b], sa = a_sin[b];
+                const double dirx = ct * ca - sn * sa;  // build-defined particle pose (lp = (0,0,0) in :176)
+                const double diry = sn * ca + ct * sa;
+                double wx = px, wy = py;
+                wx += d * dirx;
+                wy += d * diry;
+                int x1, y1;
+                gm_world2map(g, wx, wy, x1, y1);
+                const bool hit = d < g.max_urange;
+                hitxy[b] = make_float2((float)wx, (float)wy);
+                // lines longer than 16383 cells are not representable (max_range / delta < 16384)
+                if (abs(x1 - x0) < GM_REL && abs(y1 - y0) < GM_REL) {
+                    r = gm_pack(x1 - x0, y1 - y0, hit);
+                    gx0 = min(gx0, x1); gy0 = min(gy0, y1); gx1 = max(gx1, x1); gy1 = max(gy1, y1);
+                    // cells outside the map are skipped (an assert in the reference, G/grid/map.h:188-191)
+                    if (hit && x1 >= 0 && x1 < g.sx && y1 >= 0 && y1 < g.sy) {
+                        const int tx = x1 / GM_TILE, ty = y1 / GM_TILE_H;
+                        if (tx >= ptx0 && tx <= ptx1 && ty >= pty0 && ty <= pty1) {
+                            const int *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
+                            const int c = (y1 % GM_TILE_H) * GM_TILE + (x1 % GM_TILE);
+                            const int vis = tp[c], nn = tp[GM_TILE_CELLS + c];
+                            const double occ = vis ? (double)nn * 1 / (double)vis : -1;  // map.h:27
+                            score += occ > g.occ_thresh ? 1 : 0;
+                        }
+                    }
+                }
+                hits += hit ? 1 : 0;
+            }
+            rays[b] = r;
+        }
+        bx0 = min(bx0, gx0); by0 = min(by0, gy0); bx1 = max(bx1, gx1); by1 = max(by1, gy1);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            gx0 = min(gx0, __shfl_xor(gx0, off, 64));
+            gy0 = min(gy0, __shfl_xor(gy0, off, 64));
+            gx1 = max(gx1, __shfl_xor(gx1, off, 64));
+            gy1 = max(gy1, __shfl_xor(gy1, off, 64));
+        }
+        if ((tid & 63) == 0) gbox[b0 >> 6] = make_int4(gx0, gy0, gx1, gy1);
+    }
+    // the written tile box: the rays' box clamped to the map
+    atomicMin(&s_box[0], max(bx0, 0)); atomicMin(&s_box[1], max(by0, 0));
+    atomicMax(&s_box[2], min(bx1, g.sx - 1)); atomicMax(&s_box[3], min(by1, g.sy - 1));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        score += __shfl_xor(score, off, 64);
+        hits += __shfl_xor(hits, off, 64);
+    }
+    if ((tid & 63) == 0) {
+        s_red[tid >> 6][0] = score;
+        s_red[tid >> 6][1] = hits;
+    }
+    __syncthreads();  // also orders every score read of the previous map before the tile writes
+
+    const bool any_cell = s_box[0] <= s_box[2] && s_box[1] <= s_box[3];
+    const int tx0 = any_cell ? s_box[0] / GM_TILE : 1, ty0 = any_cell ? s_box[1] / GM_TILE_H : 1;
+    const int tx1 = any_cell ? s_box[2] / GM_TILE : 0, ty1 = any_cell ? s_box[3] / GM_TILE_H : 0;
+    if (tid == 0) {
+        int sc = 0, hc = 0;
+        for (int w = 0; w < GM_THREADS / 64; ++w) {
+            sc += s_red[w][0];
+            hc += s_red[w][1];
+        }
+        st.score = sc;
+        st.hits = hc;
+        st.tx0 = tx0; st.ty0 = ty0; st.tx1 = tx1; st.ty1 = ty1;
+        if (scores_out) scores_out[blockIdx.x] = sc;
+    }
+
+    long long nfree = 0;
+    const int ntx = tx1 - tx0 + 1, ntiles = (tx1 >= tx0) ? ntx * (ty1 - ty0 + 1) : 0;
+    for (int t = 0; t < ntiles; ++t) {
+        const int tx = tx0 + t % ntx, ty = ty0 + t / ntx;
+        const int X0 = tx * GM_TILE, Y0 = ty * GM_TILE_H;
+        const int X1 = min(X0 + GM_TILE, g.sx), Y1 = min(Y0 + GM_TILE_H, g.sy);
+        for (int k = tid; k < GM_LDS_WORDS / 4; k += GM_THREADS) {
+            reinterpret_cast<uint4 *>(cnt)[k] = make_uint4(0u, 0u, 0u, 0u);
+            reinterpret_cast<uint4 *>(first_hit)[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+        __syncthreads();
+        for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
+            const int4 gb = gbox[b0 >> 6];
+            const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
+            const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
+            if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
+            const int b = b0 + (tid & 63);
+            if (b >= n) continue;
+            const unsigned r = rays[b];
+            if (r == GM_RAY_INVALID) continue;
+            const int x1 = x0 + (int)(r & 0xFFFFu) - GM_REL, y1 = y0 + (int)((r >> 16) & 0x7FFFu) - GM_REL;
+            if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
+            if ((r & GM_RAY_HIT) && x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {
+                const int c = (y1 - Y0) * GM_STRIDE + (x1 - X0);
+                atomicAdd(&cnt[c], 0x10001u);       // n++, visits++ (map.h:40-44)
+                atomicMin(&first_hit[c], (unsigned)b);
+            }
+            const GmLine l = gm_line(x0, y0, x1, y1);
+            int lo = l.ilo, hi = l.ihi;
+            const bool in = l.x_major ? gm_clip(l, X0, X1, Y0, Y1, lo, hi) : gm_clip(l, Y0, Y1, X0, X1, lo, hi);
+            if (!in) continue;
+            const unsigned two_da = 2u * (unsigned)l.da, two_db = 2u * (unsigned)l.db;
+            const unsigned num = two_db * (unsigned)lo + (unsigned)l.da;
+            const int q = l.da ? (int)(num / two_da) : 0;
+            unsigned rem = num - (unsigned)q * two_da;
+            const int la = l.x_major ? 1 : GM_STRIDE, lb = l.x_major ? GM_STRIDE : 1;
+            const int A0 = l.x_major ? X0 : Y0, B0 = l.x_major ? Y0 : X0;
+            int li = (l.as + lo - A0) * la + (l.bs + l.sb * q - B0) * lb;
+            const int db_step = l.sb * lb;
+            nfree += hi - lo + 1;
+            for (int i = lo; i <= hi; ++i) {
+                atomicAdd(&cnt[li], 1u);              // visits++ (:227-234)
+                li += la;
+                rem += two_db;
+                if (rem >= two_da) {
+                    rem -= two_da;
+                    li += db_step;
+                }
+            }
+        }
+        __syncthreads();
+        int *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
+        float *accx = reinterpret_cast<float *>(tp + 2 * GM_TILE_CELLS);
+        float *accy = reinterpret_cast<float *>(tp + 3 * GM_TILE_CELLS);
+        // acc: the first hitting beam of a cell sums every hit of that cell in beam order (:236-240)
+        for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
+            const int b = b0 + (tid & 63);
+            if (b >= n) continue;
+            const unsigned r = rays[b];
+            if (r == GM_RAY_INVALID || !(r & GM_RAY_HIT)) continue;
+            const int x1 = x0 + (int)(r & 0xFFFFu) - GM_REL, y1 = y0 + (int)((r >> 16) & 0x7FFFu) - GM_REL;
+            if (x1 < X0 || x1 >= X1 || y1 < Y0 || y1 >= Y1) continue;
+            const int c = (y1 - Y0) * GM_STRIDE + (x1 - X0);
+            if (first_hit[c] != (unsigned)b) continue;
+            float ax = 0.0f, ay = 0.0f;
+            ax += hitxy[b].x;
+            ay += hitxy[b].y;
+            if ((cnt[c] >> 16) > 1) {
+                for (int b2 = b + 1; b2 < n; ++b2)
+                    if (rays[b2] == r) {
+                        ax += hitxy[b2].x;
+                        ay += hitxy[b2].y;
+                    }
+            }
+            const int o = (y1 - Y0) * GM_TILE + (x1 - X0);
+            accx[o] = ax;
+            accy[o] = ay;
+        }
+        // counts: whole tile (a fresh map: untouched cells written as zero)
+        for (int qi = tid; qi < GM_TILE_CELLS / 4; qi += GM_THREADS) {
+            const int row = qi >> 4, c4 = (qi & 15) << 2;
+            const uint4 cv = *reinterpret_cast<const uint4 *>(&cnt[row * GM_STRIDE + c4]);
+            const int o = row * GM_TILE + c4;
+            *reinterpret_cast<int4 *>(&tp[o]) =
+                make_int4((int)(cv.x & 0xFFFFu), (int)(cv.y & 0xFFFFu), (int)(cv.z & 0xFFFFu), (int)(cv.w & 0xFFFFu));
+            *reinterpret_cast<int4 *>(&tp[GM_TILE_CELLS + o]) =
+                make_int4((int)(cv.x >> 16), (int)(cv.y >> 16), (int)(cv.z >> 16), (int)(cv.w >> 16));
+            if ((cv.x | cv.y | cv.z | cv.w) < 0x10000u) {  // no hit in the quad
+                *reinterpret_cast<float4 *>(&accx[o]) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                *reinterpret_cast<float4 *>(&accy[o]) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            } else {
+                if (cv.x < 0x10000u) { accx[o] = 0.0f; accy[o] = 0.0f; }
+                if (cv.y < 0x10000u) { accx[o + 1] = 0.0f; accy[o + 1] = 0.0f; }
+                if (cv.z < 0x10000u) { accx[o + 2] = 0.0f; accy[o + 2] = 0.0f; }
+                if (cv.w < 0x10000u) { accx[o + 3] = 0.0f; accy[o + 3] = 0.0f; }
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) nfree += __shfl_xor(nfree, off, 64);
+    __shared__ long long s_free[GM_THREADS / 64];
+    if ((tid & 63) == 0) s_free[tid >> 6] = nfree;
+    __syncthreads();
+    if (tid == 0) {
+        long long f = 0;
+        for (int w = 0; w < GM_THREADS / 64; ++w) f += s_free[w];
+        st.free_updates = f;
+    }
+}
+
+// GMapping::PublishMap conversion (gmapping.cc:141-159): -1 unvisited, 100 if n/visits > thresh, 0
+__global__ void gm_publish_kernel(const int *__restrict__ pm, GmGeom g, GmState st, int8_t *__restrict__ out)
+{
+    const size_t total = (size_t)g.sx * g.sy;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int x = (int)(i % g.sx), y = (int)(i / g.sx);
+        const int tx = x / GM_TILE, ty = y / GM_TILE_H;
+        int vis = 0, nn = 0;
+        if (tx >= st.tx0 && tx <= st.tx1 && ty >= st.ty0 && ty <= st.ty1) {
+            const int *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
+            const int c = (y % GM_TILE_H) * GM_TILE + (x % GM_TILE);
+            vis = tp[c];
+            nn = tp[GM_TILE_CELLS + c];
+        }
+        const double occ = vis ? (double)nn * 1 / (double)vis : -1;
+        out[i] = occ < 0 ? (int8_t)-1 : (occ > g.occ_thresh ? (int8_t)100 : (int8_t)0);
+    }
+}
+
+}  // namespace s2d

@@ -59,23 +59,23 @@ def _declare(L):
     L.hs_get_stream.argtypes = [_p]
     L.hs_set_timing.argtypes = [_p, _i]
     L.hs_get_kernel_times.argtypes = [_p, _p, _p, _i]
-    # GMapping particle path
-    if hasattr(L, "gm_create"):
-        L.gm_version.restype = C.c_char_p
-        L.gm_create.argtypes = [P(_p), _i, _i, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
-                                C.c_double, C.c_double, C.c_double]
-        L.gm_destroy.argtypes = [_p]
-        L.gm_set_beams.argtypes = [_p, _p, _p, _i]
-        L.gm_compute_maps.argtypes = [_p, _p, _p, _i, _p]
-        L.gm_compute_maps_device.argtypes = [_p, _p, _p, _i, _i, _p]
-        L.gm_get_particle_map.argtypes = [_p, _i, _p, _p, _p, _p]
-        L.gm_get_weights.argtypes = [_p, _p, _p]
-        L.gm_get_device_weights.restype = _p
-        L.gm_get_device_weights.argtypes = [_p]
-        L.gm_get_stats.argtypes = [_p, _p]
-        L.gm_set_timing.argtypes = [_p, _i]
-        L.gm_get_kernel_times.argtypes = [_p, _p, _p, _i]
-        L.gm_get_map_size.argtypes = [_p, P(_i), P(_i)]
+    # GMapping particle path (include/slam2d/gmapping.h)
+    D = C.c_double
+    L.gm_version.restype = C.c_char_p
+    L.gm_last_error.restype = C.c_char_p
+    L.gm_create.argtypes = [P(_p), _i, _i, D, D, D, D, D, D, D]
+    L.gm_destroy.argtypes = [_p]
+    L.gm_reset.argtypes = [_p]
+    L.gm_set_beams.argtypes = [_p, _p, _p, _i]
+    L.gm_set_occ_thresh.argtypes = [_p, D]
+    L.gm_get_map_size.argtypes = [_p, P(_i), P(_i)]
+    L.gm_compute_maps.argtypes = [_p, _p, _p, _i]
+    L.gm_compute_maps_device.argtypes = [_p, _i, _i, _p, _p, _i, _p, _p]
+    L.gm_get_particle_map.argtypes = [_p, _i, _p, _p, _p]
+    L.gm_publish.argtypes = [_p, _i, _p]
+    L.gm_get_scores.argtypes = [_p, _p, _p, _p]
+    L.gm_set_timing.argtypes = [_p, _i]
+    L.gm_get_kernel_times.argtypes = [_p, _p, _p, _i]
 
 
 def lib() -> C.CDLL:

@@ -1,0 +1,144 @@
+"""GMapping particle-map path over the MI355X C-ABI (include/slam2d/gmapping.h).
+
+Reference: lesson4 `make_gmapping_map` -- GMapping::ComputeMap (lesson4/src/gmapping/gmapping.cc:
+171-242) into a fresh ScanMatcherMap per scan, PublishMap (:141-159), CreateCache (:111-124).
+`GMappingFleet` evaluates one scan for P candidate poses ("particles") resident on one GPU; the
+particles of a multi-GPU job are sharded over ranks and their scores normalised with one RCCL
+all-reduce (`normalize_weights`).  Every compute call goes to the HIP library; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import Slam2dError
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _check(L, rc: int, what: str):
+    if rc != 0:
+        raise Slam2dError(f"{what} failed with code {rc}: {L.gm_last_error().decode(errors='replace')}")
+
+
+# gmapping.cc ctor defaults / launch parameters: +-40 m map at 0.05 m,
+# maxRange 30 - 0.01, maxUrange 25, occ_thresh 0.25
+DEFAULTS = dict(xmin=-40.0, ymin=-40.0, xmax=40.0, ymax=40.0, delta=0.05, max_range=30.0 - 0.01, max_urange=25.0)
+
+
+class GMappingFleet:
+    """P particle maps of GMapping::ComputeMap on one GPU."""
+
+    def __init__(self, num_particles: int, max_beams: int = 1081, **params):
+        p = dict(DEFAULTS)
+        p.update(params)
+        self.L = _lib.lib()
+        self.P = num_particles
+        self.h = C.c_void_p()
+        _check(self.L, self.L.gm_create(C.byref(self.h), num_particles, max_beams, p["xmin"], p["ymin"], p["xmax"],
+                                        p["ymax"], p["delta"], p["max_range"], p["max_urange"]), "gm_create")
+        sx, sy = C.c_int(), C.c_int()
+        self.L.gm_get_map_size(self.h, C.byref(sx), C.byref(sy))
+        self.size = (sx.value, sy.value)
+        self.n_beams = 0
+
+    def close(self):
+        if self.h:
+            self.L.gm_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        _check(self.L, self.L.gm_reset(self.h), "gm_reset")
+
+    def set_beams(self, angles=None, a_cos=None, a_sin=None):
+        """GMapping::CreateCache (gmapping.cc:111-124): cos/sin of every beam angle (double)."""
+        if angles is not None:
+            angles = np.asarray(angles, np.float64)
+            a_cos, a_sin = np.cos(angles), np.sin(angles)
+        a_cos = np.ascontiguousarray(a_cos, np.float64)
+        a_sin = np.ascontiguousarray(a_sin, np.float64)
+        _check(self.L, self.L.gm_set_beams(self.h, _fp(a_cos), _fp(a_sin), a_cos.shape[0]), "gm_set_beams")
+        self.n_beams = a_cos.shape[0]
+
+    def set_occ_thresh(self, t: float):
+        _check(self.L, self.L.gm_set_occ_thresh(self.h, float(t)), "gm_set_occ_thresh")
+
+    @staticmethod
+    def poses4(poses_xyt) -> np.ndarray:
+        """(x, y, theta) -> (x, y, cos theta, sin theta) as the kernel consumes them."""
+        p = np.asarray(poses_xyt, np.float64).reshape(-1, 3)
+        return np.ascontiguousarray(np.stack([p[:, 0], p[:, 1], np.cos(p[:, 2]), np.sin(p[:, 2])], axis=1))
+
+    def compute(self, poses4, ranges):
+        """ComputeMap for every particle (host arrays, synchronous)."""
+        poses4 = np.ascontiguousarray(poses4, np.float64).reshape(self.P, 4)
+        ranges = np.ascontiguousarray(ranges, np.float32)
+        _check(self.L, self.L.gm_compute_maps(self.h, _fp(poses4), _fp(ranges), ranges.shape[0]), "gm_compute_maps")
+
+    def compute_device(self, d_poses4: int, d_ranges: int, n: int, d_scores: int = 0, begin: int = 0,
+                       count: int | None = None, hip_stream: int = 0):
+        count = self.P - begin if count is None else count
+        _check(self.L, self.L.gm_compute_maps_device(self.h, begin, count, C.c_void_p(d_poses4), C.c_void_p(d_ranges),
+                                                     int(n), C.c_void_p(d_scores or None),
+                                                     C.c_void_p(hip_stream or None)), "gm_compute_maps_device")
+
+    def particle_map(self, p: int):
+        sx, sy = self.size
+        n = np.empty(sx * sy, np.int32)
+        v = np.empty(sx * sy, np.int32)
+        acc = np.empty(2 * sx * sy, np.float32)
+        _check(self.L, self.L.gm_get_particle_map(self.h, p, _fp(n), _fp(v), _fp(acc)), "gm_get_particle_map")
+        return n.reshape(sy, sx), v.reshape(sy, sx), acc.reshape(sy, sx, 2)
+
+    def publish(self, p: int) -> np.ndarray:
+        sx, sy = self.size
+        o = np.empty(sx * sy, np.int8)
+        _check(self.L, self.L.gm_publish(self.h, p, _fp(o)), "gm_publish")
+        return o.reshape(sy, sx)
+
+    def scores(self):
+        s = np.empty(self.P, np.int32)
+        h = np.empty(self.P, np.int32)
+        f = np.empty(self.P, np.int64)
+        _check(self.L, self.L.gm_get_scores(self.h, _fp(s), _fp(h), _fp(f)), "gm_get_scores")
+        return s, h, f
+
+    def set_timing(self, on: bool):
+        _check(self.L, self.L.gm_set_timing(self.h, 1 if on else 0), "gm_set_timing")
+
+    def kernel_times(self, reset=True):
+        ms = C.c_double()
+        n = C.c_int64()
+        _check(self.L, self.L.gm_get_kernel_times(self.h, C.byref(ms), C.byref(n), 1 if reset else 0),
+               "gm_get_kernel_times")
+        return ms.value, n.value
+
+
+def normalize_weights(scores, group=None):
+    """Particle weights from the particles' integer scores, across every rank that holds particles:
+    w_p = (score_p + 1) / Σ_all (score_q + 1)  (the +1 keeps a particle with no agreeing hit alive).
+
+    The exchange is ONE all-reduce of [Σ(score+1), Σ(score+1)^2] (RCCL on the GPU box, gloo in the
+    CPU tests); returns (local weights as float64 tensor, effective sample size of the whole set).
+    `scores` is a torch int tensor of this rank's particles (device or CPU)."""
+    import torch
+    import torch.distributed as dist
+
+    s = scores.to(torch.float64) + 1.0
+    red = torch.stack([s.sum(), (s * s).sum()])
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=group)
+    total, sq = red[0], red[1]
+    w = s / total
+    neff = (total * total) / sq
+    return w, float(neff)

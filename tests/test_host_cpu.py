@@ -142,3 +142,38 @@ def test_rank_aggregation_single_process():
     import torch
 
     assert bench.aggregate_over_ranks(0.5, 7.0, torch.device("cpu")) == (0.5, 7.0)
+
+
+# ----------------------------------------------------------------------------- GMapping weight exchange (gloo)
+def _weights_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+
+    from slam2d.gmapping import normalize_weights
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    scores = torch.arange(rank * 3, rank * 3 + 3, dtype=torch.int32)   # this rank's particle shard
+    w, neff = normalize_weights(scores)
+    out[rank] = (w.tolist(), neff)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_particle_weight_allreduce_gloo_world2():
+    """Sharded particles: one all-reduce gives weights identical to the single-process result."""
+    import torch
+    import torch.multiprocessing as mp
+
+    from slam2d.gmapping import normalize_weights
+
+    world = 2
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_weights_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    w_all, neff_all = normalize_weights(torch.arange(0, 6, dtype=torch.int32))
+    got = res[0][0] + res[1][0]
+    np.testing.assert_allclose(got, w_all.tolist(), rtol=0, atol=0)
+    assert abs(sum(got) - 1.0) < 1e-12
+    assert res[0][1] == res[1][1] == neff_all

@@ -37,8 +37,11 @@ int gfail(int code, const char *what, hipError_t e = hipSuccess)
 
 struct gm_ctx {
     int P = 0, max_beams = 0, n_beams = 0;
+    int parts = 2;  // gm_compute_kernel workgroups per particle (SLAM2D_GM_PARTS)
     GmGeom geom{};
-    int *d_maps = nullptr;
+    unsigned *d_maps = nullptr;   // packed counts, tiled
+    int *d_stamps = nullptr;      // per particle, per tile
+    GmHitCell *d_hits = nullptr;  // per particle, max_beams entries
     GmState *d_state = nullptr;
     double *d_cos = nullptr, *d_sin = nullptr;
     double *d_poses = nullptr;  // host-pointer staging
@@ -62,10 +65,11 @@ int reset_state(gm_ctx *c)
 {
     std::vector<GmState> h(c->P);
     for (auto &s : h) {
+        memset(&s, 0, sizeof(s));
         s.tx0 = 1; s.ty0 = 1; s.tx1 = 0; s.ty1 = 0;  // empty box: a fresh map
-        s.score = 0; s.hits = 0; s.free_updates = 0;
     }
     GCHK(hipMemcpy(c->d_state, h.data(), sizeof(GmState) * c->P, hipMemcpyHostToDevice));
+    GCHK(hipMemset(c->d_stamps, 0, sizeof(int) * (size_t)c->geom.ntiles * c->P));
     return GM_OK;
 }
 
@@ -84,8 +88,12 @@ int launch(gm_ctx *c, int begin, int count, const double *d_poses, const float *
         }
         GCHK(hipEventRecord(ev.first, s));
     }
-    hipLaunchKernelGGL(gm_compute_kernel, dim3(count), dim3(GM_THREADS), gm_shmem(n), s, c->geom, d_poses, d_ranges, n,
-                       c->d_cos, c->d_sin, c->d_maps, c->d_state, d_scores, begin);
+    hipLaunchKernelGGL(gm_score_kernel, dim3(count), dim3(GM_THREADS), 0, s, c->geom, d_poses, d_ranges, n, c->d_cos,
+                       c->d_sin, c->d_maps, c->d_stamps, c->d_state, d_scores, begin);
+    GCHK(hipGetLastError());
+    hipLaunchKernelGGL(gm_compute_kernel, dim3(count * c->parts), dim3(GM_THREADS), gm_shmem(n), s, c->geom, d_poses,
+                       d_ranges, n, c->d_cos, c->d_sin, c->d_maps, c->d_stamps, c->d_hits, c->d_state, begin, count,
+                       c->parts);
     GCHK(hipGetLastError());
     if (c->timing) {
         GCHK(hipEventRecord(ev.second, s));
@@ -112,6 +120,7 @@ int gm_create(gm_ctx **out, int num_particles, int max_beams, double xmin, doubl
     gm_ctx *c = new gm_ctx;
     c->P = num_particles;
     c->max_beams = max_beams;
+    if (const char *e2 = getenv("SLAM2D_GM_PARTS")) c->parts = atoi(e2) < 1 ? 1 : (atoi(e2) > 16 ? 16 : atoi(e2));
     GmGeom &g = c->geom;
     // ScanMatcherMap / HierarchicalArray2D geometry (G/grid/map.h:133-143, harray2d.h: 32-cell patches)
     g.cx = (xmin + xmax) / 2.0;
@@ -132,12 +141,15 @@ int gm_create(gm_ctx **out, int num_particles, int max_beams, double xmin, doubl
     g.tiles_x = (g.sx + GM_TILE - 1) / GM_TILE;
     g.tiles_y = (g.sy + GM_TILE_H - 1) / GM_TILE_H;
     g.particle_words = (size_t)g.tiles_x * g.tiles_y * GM_TILE_BLOCK_WORDS;
+    g.ntiles = g.tiles_x * g.tiles_y;
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         return gfail(GM_EHIP, "hipStreamCreate", e);
     }
-    if ((e = hipMalloc(&c->d_maps, sizeof(int) * g.particle_words * (size_t)c->P)) != hipSuccess ||
+    if ((e = hipMalloc(&c->d_maps, sizeof(unsigned) * g.particle_words * (size_t)c->P)) != hipSuccess ||
+        (e = hipMalloc(&c->d_stamps, sizeof(int) * (size_t)g.ntiles * c->P)) != hipSuccess ||
+        (e = hipMalloc(&c->d_hits, sizeof(GmHitCell) * (size_t)max_beams * c->P)) != hipSuccess ||
         (e = hipMalloc(&c->d_state, sizeof(GmState) * c->P)) != hipSuccess ||
         (e = hipMalloc(&c->d_cos, sizeof(double) * max_beams)) != hipSuccess ||
         (e = hipMalloc(&c->d_sin, sizeof(double) * max_beams)) != hipSuccess ||
@@ -161,6 +173,8 @@ int gm_destroy(gm_ctx *c)
     if (!c) return GM_OK;
     if (c->stream) hipStreamSynchronize(c->stream);
     hipFree(c->d_maps);
+    hipFree(c->d_stamps);
+    hipFree(c->d_hits);
     hipFree(c->d_state);
     hipFree(c->d_cos);
     hipFree(c->d_sin);
@@ -239,13 +253,16 @@ int gm_get_particle_map(gm_ctx *c, int p, int32_t *n_out, int32_t *visits_out, f
     if (n_out) memset(n_out, 0, sizeof(int32_t) * cells);
     if (visits_out) memset(visits_out, 0, sizeof(int32_t) * cells);
     if (acc_out) memset(acc_out, 0, sizeof(float) * 2 * cells);
-    if (st.tx1 < st.tx0) return GM_OK;
-    std::vector<int> tile(GM_TILE_BLOCK_WORDS);
-    const int *pm = c->d_maps + (size_t)p * g.particle_words;
+    if (st.step == 0 || st.tx1 < st.tx0) return GM_OK;
+    std::vector<int> stamps(g.ntiles);
+    GCHK(hipMemcpy(stamps.data(), c->d_stamps + (size_t)p * g.ntiles, sizeof(int) * g.ntiles, hipMemcpyDeviceToHost));
+    std::vector<unsigned> tile(GM_TILE_BLOCK_WORDS);
+    const unsigned *pm = c->d_maps + (size_t)p * g.particle_words;
     for (int ty = st.ty0; ty <= st.ty1; ++ty)
         for (int tx = st.tx0; tx <= st.tx1; ++tx) {
+            if (stamps[ty * g.tiles_x + tx] != st.step) continue;  // not written this step: fresh
             GCHK(hipMemcpy(tile.data(), pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS,
-                           sizeof(int) * GM_TILE_BLOCK_WORDS, hipMemcpyDeviceToHost));
+                           sizeof(unsigned) * GM_TILE_BLOCK_WORDS, hipMemcpyDeviceToHost));
             for (int r = 0; r < GM_TILE_H; ++r) {
                 const int y = ty * GM_TILE_H + r;
                 if (y >= g.sy) break;
@@ -253,16 +270,21 @@ int gm_get_particle_map(gm_ctx *c, int p, int32_t *n_out, int32_t *visits_out, f
                     const int x = tx * GM_TILE + k;
                     if (x >= g.sx) break;
                     const size_t o = (size_t)y * g.sx + x;
-                    const int cidx = r * GM_TILE + k;
-                    if (visits_out) visits_out[o] = tile[cidx];
-                    if (n_out) n_out[o] = tile[GM_TILE_CELLS + cidx];
-                    if (acc_out) {
-                        memcpy(&acc_out[2 * o], &tile[2 * GM_TILE_CELLS + cidx], sizeof(float));
-                        memcpy(&acc_out[2 * o + 1], &tile[3 * GM_TILE_CELLS + cidx], sizeof(float));
-                    }
+                    const unsigned cv = tile[r * GM_TILE + k];
+                    if (visits_out) visits_out[o] = (int32_t)(cv & 0xFFFFu);
+                    if (n_out) n_out[o] = (int32_t)(cv >> 16);
                 }
             }
         }
+    if (acc_out && st.hit_cells > 0) {
+        std::vector<GmHitCell> hits(st.hit_cells);
+        GCHK(hipMemcpy(hits.data(), c->d_hits + (size_t)p * c->max_beams, sizeof(GmHitCell) * st.hit_cells,
+                       hipMemcpyDeviceToHost));
+        for (const auto &h : hits) {
+            acc_out[2 * (size_t)h.cell] = h.ax;
+            acc_out[2 * (size_t)h.cell + 1] = h.ay;
+        }
+    }
     return GM_OK;
 }
 
@@ -273,7 +295,7 @@ int gm_publish(gm_ctx *c, int p, int8_t *occ_out)
     GmState st;
     GCHK(hipMemcpy(&st, c->d_state + p, sizeof(GmState), hipMemcpyDeviceToHost));
     hipLaunchKernelGGL(gm_publish_kernel, dim3(1024), dim3(256), 0, c->stream, c->d_maps + (size_t)p * c->geom.particle_words,
-                       c->geom, st, c->d_occ);
+                       c->d_stamps + (size_t)p * c->geom.ntiles, c->geom, st.step, c->d_occ);
     GCHK(hipGetLastError());
     GCHK(hipMemcpyAsync(occ_out, c->d_occ, (size_t)c->geom.sx * c->geom.sy, hipMemcpyDeviceToHost, c->stream));
     GCHK(hipStreamSynchronize(c->stream));

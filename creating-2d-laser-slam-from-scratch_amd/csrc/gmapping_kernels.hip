@@ -1,9 +1,11 @@
 // gmapping_kernels.hip -- MI355X kernels of the GMapping particle-map path (config 4).
 //
-//   gm_compute_kernel   one 256-thread workgroup per particle: GMapping::ComputeMap
+//   gm_score_kernel     one workgroup per particle: the particle's score of the new scan against its
+//                       previous map (read before it is overwritten); opens the particle's new step.
+//   gm_compute_kernel   `parts` 256-thread workgroups per particle: GMapping::ComputeMap
 //                       (lesson4/src/gmapping/gmapping.cc:171-242) of the shared scan seen from the
-//                       particle's pose, into the particle's tiled (n, visits, acc) map, plus the
-//                       particle's score against its previous map (read before it is overwritten).
+//                       particle's pose, into the particle's tiled packed-count map (part q draws
+//                       tiles q, q + parts, ...) and its list of hit cells with their accumulators.
 //
 // Raster: GridLineTraversal::gridLine (lesson4/include/lesson4/gmapping/grid/gridlinetraversal.h:
 // 27-207) starts at the endpoint with the smaller major coordinate and, with decision variable
@@ -21,6 +23,20 @@
 #include "gmapping_internal.h"
 
 namespace s2d {
+
+// n / d for n < 2^31, 1 <= d < 2^16, exact when the quotient is < 2^16 (see hector_kernels.hip
+// udiv_small; larger quotients only ever mean "beyond the line")
+__device__ __forceinline__ unsigned gm_udiv(unsigned n, unsigned d)
+{
+    unsigned q = (unsigned)((float)n * __builtin_amdgcn_rcpf((float)d));
+    int r = (int)(n - q * d);
+    if (r < 0) {
+        --q;
+        r += (int)d;
+    }
+    if (r >= (int)d) ++q;
+    return q;
+}
 
 constexpr int GM_STRIDE = 68;                          // LDS words per tile row (16-B rows)
 constexpr int GM_LDS_WORDS = GM_TILE_H * GM_STRIDE;    // one LDS tile array
@@ -80,19 +96,113 @@ __device__ __forceinline__ bool gm_clip(const GmLine &l, int A0, int A1, int B0,
     const unsigned two_da = 2u * (unsigned)l.da, two_db = 2u * (unsigned)l.db;
     if (tlo > 0) {  // smallest i with q(i) >= tlo
         const unsigned x = two_da * (unsigned)tlo - (unsigned)l.da;
-        lo = max(lo, (int)((x + two_db - 1u) / two_db));
+        lo = max(lo, (int)gm_udiv(x + two_db - 1u, two_db));
     }
     {  // largest i with q(i) <= thi
         const unsigned y = two_da * (unsigned)(thi + 1) - (unsigned)l.da;
-        hi = min(hi, (int)((y - 1u) / two_db));
+        hi = min(hi, (int)gm_udiv(y - 1u, two_db));
     }
     return lo <= hi;
 }
 
+// One beam of ComputeMap (:185-214): validity filter, clamp to maxUrange, end point in double.
+struct GmBeam {
+    bool valid, hit;
+    int x1, y1;
+    double wx, wy;
+};
+
+__device__ __forceinline__ GmBeam gm_beam(const GmGeom &g, double px, double py, double ct, double sn, float range,
+                                          double ca, double sa)
+{
+    GmBeam e;
+    double d = range;
+    e.valid = !(d > g.max_range || d == 0.0 || !isfinite(d));
+    e.hit = false;
+    e.x1 = e.y1 = 0;
+    e.wx = e.wy = 0.0;
+    if (!e.valid) return e;
+    if (d > g.max_urange) d = g.max_urange;
+    const double dirx = ct * ca - sn * sa;  // build-defined particle pose (lp = (0,0,0) in :176)
+    const double diry = sn * ca + ct * sa;
+    double wx = px, wy = py;
+    wx += d * dirx;
+    wy += d * diry;
+    gm_world2map(g, wx, wy, e.x1, e.y1);
+    e.hit = d < g.max_urange;
+    e.wx = wx;
+    e.wy = wy;
+    return e;
+}
+
+// Particle weight (build-defined, the reference has no particles): hit beams of this scan whose
+// end cell is occupied (n/visits > occ_thresh, map.h:27 + gmapping.cc:150) in the particle's
+// previous map.  Runs before gm_compute_kernel overwrites that map; opens the particle's new step.
+__global__ void __launch_bounds__(GM_THREADS)
+gm_score_kernel(GmGeom g, const double *__restrict__ poses, const float *__restrict__ ranges, int n,
+                const double *__restrict__ a_cos, const double *__restrict__ a_sin, const unsigned *__restrict__ maps,
+                const int *__restrict__ stamps, GmState *__restrict__ state, int *__restrict__ scores_out,
+                int particle_begin)
+{
+    __shared__ int s_red[GM_THREADS / 64][2];
+    const int p = particle_begin + blockIdx.x;
+    const int tid = threadIdx.x;
+    const unsigned *pm = maps + (size_t)p * g.particle_words;
+    const int *pstamp = stamps + (size_t)p * g.ntiles;
+    GmState &st = state[p];
+    const int prev_step = st.step;
+    const int ptx0 = st.tx0, pty0 = st.ty0, ptx1 = st.tx1, pty1 = st.ty1;  // previous map's box
+    const double px = poses[4 * blockIdx.x], py = poses[4 * blockIdx.x + 1];
+    const double ct = poses[4 * blockIdx.x + 2], sn = poses[4 * blockIdx.x + 3];
+    int score = 0, hits = 0;
+    for (int b = tid; b < n; b += GM_THREADS) {
+        const GmBeam e = gm_beam(g, px, py, ct, sn, ranges[b], a_cos[b], a_sin[b]);
+        if (!e.valid || !e.hit) continue;
+        hits += 1;
+        const int x1 = e.x1, y1 = e.y1;
+        if (prev_step > 0 && x1 >= 0 && x1 < g.sx && y1 >= 0 && y1 < g.sy) {
+            const int tx = x1 / GM_TILE, ty = y1 / GM_TILE_H;
+            if (tx >= ptx0 && tx <= ptx1 && ty >= pty0 && ty <= pty1 && pstamp[ty * g.tiles_x + tx] == prev_step) {
+                const unsigned cv = pm[(size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS + (y1 % GM_TILE_H) * GM_TILE +
+                                       (x1 % GM_TILE)];
+                const int vis = (int)(cv & 0xFFFFu), nn = (int)(cv >> 16);
+                const double occ = vis ? (double)nn * 1 / (double)vis : -1;
+                score += occ > g.occ_thresh ? 1 : 0;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        score += __shfl_xor(score, off, 64);
+        hits += __shfl_xor(hits, off, 64);
+    }
+    if ((tid & 63) == 0) {
+        s_red[tid >> 6][0] = score;
+        s_red[tid >> 6][1] = hits;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int sc = 0, hc = 0;
+        for (int w = 0; w < GM_THREADS / 64; ++w) {
+            sc += s_red[w][0];
+            hc += s_red[w][1];
+        }
+        st.score = sc;
+        st.hits = hc;
+        st.step = prev_step + 1;   // tiles stamped with this step form the new map
+        st.free_updates = 0;
+        st.hit_cells = 0;
+        if (scores_out) scores_out[blockIdx.x] = sc;
+    }
+}
+
+// Grid: parts x count workgroups (part-major); part q draws tiles q, q + parts, ... of the particle's
+// tile box.  Runs after gm_score_kernel of the same step.
 __global__ void __launch_bounds__(GM_THREADS)
 gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__restrict__ ranges, int n,
-                  const double *__restrict__ a_cos, const double *__restrict__ a_sin, int *__restrict__ maps,
-                  GmState *__restrict__ state, int *__restrict__ scores_out, int particle_begin)
+                  const double *__restrict__ a_cos, const double *__restrict__ a_sin, unsigned *__restrict__ maps,
+                  int *__restrict__ stamps, GmHitCell *__restrict__ hit_cells, GmState *__restrict__ state,
+                  int particle_begin, int count, int parts)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned smem[];
     unsigned *cnt = smem;                              // n << 16 | visits per cell of the tile
@@ -101,60 +211,40 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
     float2 *hitxy = reinterpret_cast<float2 *>(rays + ((n + 3) & ~3));   // (float)hit point
     int4 *gbox = reinterpret_cast<int4 *>(hitxy + ((n + 1) & ~1));      // per 64-beam fan group
     __shared__ int s_box[4];
-    __shared__ int s_red[GM_THREADS / 64][2];
 
-    const int p = particle_begin + blockIdx.x;
+    const int part = blockIdx.x / count;
+    const int local = blockIdx.x - part * count;
+    const int p = particle_begin + local;
     const int tid = threadIdx.x;
-    int *pm = maps + (size_t)p * g.particle_words;
+    unsigned *pm = maps + (size_t)p * g.particle_words;
+    int *pstamp = stamps + (size_t)p * g.ntiles;
+    GmHitCell *phits = hit_cells + (size_t)p * g.max_beams;
     GmState &st = state[p];
-    const double px = poses[4 * blockIdx.x], py = poses[4 * blockIdx.x + 1];
-    const double ct = poses[4 * blockIdx.x + 2], sn = poses[4 * blockIdx.x + 3];
+    const int cur_step = st.step;
+    const double px = poses[4 * local], py = poses[4 * local + 1];
+    const double ct = poses[4 * local + 2], sn = poses[4 * local + 3];
     int x0, y0;
     gm_world2map(g, px, py, x0, y0);  // p0 = world2map(lp) (:176-179)
-    const int ptx0 = st.tx0, pty0 = st.ty0, ptx1 = st.tx1, pty1 = st.ty1;  // previous map's box
 
     if (tid == 0) {
         s_box[0] = g.sx; s_box[1] = g.sy; s_box[2] = -1; s_box[3] = -1;
     }
     __syncthreads();
-    // ---- rays (:185-214) + score against the previous map
+    // ---- rays (:185-214)
     int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
-    int score = 0, hits = 0;
     for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
         const int b = b0 + (tid & 63);
         unsigned r = GM_RAY_INVALID;
         int gx0 = x0, gy0 = y0, gx1 = x0, gy1 = y0;
         if (b < n) {
-            double d = ranges[b];
-            if (!(d > g.max_range || d == 0.0 || !isfinite(d))) {
-                if (d > g.max_urange) d = g.max_urange;
-                const double ca = a_cos[b], sa = a_sin[b];
-                const double dirx = ct * ca - sn * sa;  // build-defined particle pose (lp = (0,0,0) in :176)
-                const double diry = sn * ca + ct * sa;
-                double wx = px, wy = py;
-                wx += d * dirx;
-                wy += d * diry;
-                int x1, y1;
-                gm_world2map(g, wx, wy, x1, y1);
-                const bool hit = d < g.max_urange;
-                hitxy[b] = make_float2((float)wx, (float)wy);
+            const GmBeam e = gm_beam(g, px, py, ct, sn, ranges[b], a_cos[b], a_sin[b]);
+            if (e.valid) {
+                hitxy[b] = make_float2((float)e.wx, (float)e.wy);
                 // lines longer than 16383 cells are not representable (max_range / delta < 16384)
-                if (abs(x1 - x0) < GM_REL && abs(y1 - y0) < GM_REL) {
-                    r = gm_pack(x1 - x0, y1 - y0, hit);
-                    gx0 = min(gx0, x1); gy0 = min(gy0, y1); gx1 = max(gx1, x1); gy1 = max(gy1, y1);
-                    // cells outside the map are skipped (an assert in the reference, G/grid/map.h:188-191)
-                    if (hit && x1 >= 0 && x1 < g.sx && y1 >= 0 && y1 < g.sy) {
-                        const int tx = x1 / GM_TILE, ty = y1 / GM_TILE_H;
-                        if (tx >= ptx0 && tx <= ptx1 && ty >= pty0 && ty <= pty1) {
-                            const int *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
-                            const int c = (y1 % GM_TILE_H) * GM_TILE + (x1 % GM_TILE);
-                            const int vis = tp[c], nn = tp[GM_TILE_CELLS + c];
-                            const double occ = vis ? (double)nn * 1 / (double)vis : -1;  // map.h:27
-                            score += occ > g.occ_thresh ? 1 : 0;
-                        }
-                    }
+                if (abs(e.x1 - x0) < GM_REL && abs(e.y1 - y0) < GM_REL) {
+                    r = gm_pack(e.x1 - x0, e.y1 - y0, e.hit);
+                    gx0 = min(gx0, e.x1); gy0 = min(gy0, e.y1); gx1 = max(gx1, e.x1); gy1 = max(gy1, e.y1);
                 }
-                hits += hit ? 1 : 0;
             }
             rays[b] = r;
         }
@@ -171,35 +261,19 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
     // the written tile box: the rays' box clamped to the map
     atomicMin(&s_box[0], max(bx0, 0)); atomicMin(&s_box[1], max(by0, 0));
     atomicMax(&s_box[2], min(bx1, g.sx - 1)); atomicMax(&s_box[3], min(by1, g.sy - 1));
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        score += __shfl_xor(score, off, 64);
-        hits += __shfl_xor(hits, off, 64);
-    }
-    if ((tid & 63) == 0) {
-        s_red[tid >> 6][0] = score;
-        s_red[tid >> 6][1] = hits;
-    }
-    __syncthreads();  // also orders every score read of the previous map before the tile writes
+    __syncthreads();
 
     const bool any_cell = s_box[0] <= s_box[2] && s_box[1] <= s_box[3];
     const int tx0 = any_cell ? s_box[0] / GM_TILE : 1, ty0 = any_cell ? s_box[1] / GM_TILE_H : 1;
     const int tx1 = any_cell ? s_box[2] / GM_TILE : 0, ty1 = any_cell ? s_box[3] / GM_TILE_H : 0;
-    if (tid == 0) {
-        int sc = 0, hc = 0;
-        for (int w = 0; w < GM_THREADS / 64; ++w) {
-            sc += s_red[w][0];
-            hc += s_red[w][1];
-        }
-        st.score = sc;
-        st.hits = hc;
+    if (tid == 0 && part == 0) {
         st.tx0 = tx0; st.ty0 = ty0; st.tx1 = tx1; st.ty1 = ty1;
-        if (scores_out) scores_out[blockIdx.x] = sc;
     }
+    bool any_tile_marks = false;
 
     long long nfree = 0;
     const int ntx = tx1 - tx0 + 1, ntiles = (tx1 >= tx0) ? ntx * (ty1 - ty0 + 1) : 0;
-    for (int t = 0; t < ntiles; ++t) {
+    for (int t = part; t < ntiles; t += parts) {
         const int tx = tx0 + t % ntx, ty = ty0 + t / ntx;
         const int X0 = tx * GM_TILE, Y0 = ty * GM_TILE_H;
         const int X1 = min(X0 + GM_TILE, g.sx), Y1 = min(Y0 + GM_TILE_H, g.sy);
@@ -223,6 +297,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
                 const int c = (y1 - Y0) * GM_STRIDE + (x1 - X0);
                 atomicAdd(&cnt[c], 0x10001u);       // n++, visits++ (map.h:40-44)
                 atomicMin(&first_hit[c], (unsigned)b);
+                any_tile_marks = true;
             }
             const GmLine l = gm_line(x0, y0, x1, y1);
             int lo = l.ilo, hi = l.ihi;
@@ -230,13 +305,14 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
             if (!in) continue;
             const unsigned two_da = 2u * (unsigned)l.da, two_db = 2u * (unsigned)l.db;
             const unsigned num = two_db * (unsigned)lo + (unsigned)l.da;
-            const int q = l.da ? (int)(num / two_da) : 0;
+            const int q = l.da ? (int)gm_udiv(num, two_da) : 0;
             unsigned rem = num - (unsigned)q * two_da;
             const int la = l.x_major ? 1 : GM_STRIDE, lb = l.x_major ? GM_STRIDE : 1;
             const int A0 = l.x_major ? X0 : Y0, B0 = l.x_major ? Y0 : X0;
             int li = (l.as + lo - A0) * la + (l.bs + l.sb * q - B0) * lb;
             const int db_step = l.sb * lb;
             nfree += hi - lo + 1;
+            any_tile_marks = true;
             for (int i = lo; i <= hi; ++i) {
                 atomicAdd(&cnt[li], 1u);              // visits++ (:227-234)
                 li += la;
@@ -247,12 +323,16 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
                 }
             }
         }
-        __syncthreads();
-        int *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
-        float *accx = reinterpret_cast<float *>(tp + 2 * GM_TILE_CELLS);
-        float *accy = reinterpret_cast<float *>(tp + 3 * GM_TILE_CELLS);
+        // tiles without any mark are not written: their stale stamp makes them read as fresh
+        if (!__syncthreads_or(any_tile_marks)) continue;
+        any_tile_marks = false;
+        unsigned *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
         // acc: the first hitting beam of a cell sums every hit of that cell in beam order (:236-240)
         for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
+            const int4 gb = gbox[b0 >> 6];
+            const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
+            const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
+            if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
             const int b = b0 + (tid & 63);
             if (b >= n) continue;
             const unsigned r = rays[b];
@@ -271,56 +351,39 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
                         ay += hitxy[b2].y;
                     }
             }
-            const int o = (y1 - Y0) * GM_TILE + (x1 - X0);
-            accx[o] = ax;
-            accy[o] = ay;
+            GmHitCell hc;
+            hc.cell = y1 * g.sx + x1;
+            hc.ax = ax;
+            hc.ay = ay;
+            phits[atomicAdd(&st.hit_cells, 1)] = hc;
         }
-        // counts: whole tile (a fresh map: untouched cells written as zero)
+        // counts: the whole tile (a fresh map: untouched cells written as zero), 16-B stores
         for (int qi = tid; qi < GM_TILE_CELLS / 4; qi += GM_THREADS) {
             const int row = qi >> 4, c4 = (qi & 15) << 2;
-            const uint4 cv = *reinterpret_cast<const uint4 *>(&cnt[row * GM_STRIDE + c4]);
-            const int o = row * GM_TILE + c4;
-            *reinterpret_cast<int4 *>(&tp[o]) =
-                make_int4((int)(cv.x & 0xFFFFu), (int)(cv.y & 0xFFFFu), (int)(cv.z & 0xFFFFu), (int)(cv.w & 0xFFFFu));
-            *reinterpret_cast<int4 *>(&tp[GM_TILE_CELLS + o]) =
-                make_int4((int)(cv.x >> 16), (int)(cv.y >> 16), (int)(cv.z >> 16), (int)(cv.w >> 16));
-            if ((cv.x | cv.y | cv.z | cv.w) < 0x10000u) {  // no hit in the quad
-                *reinterpret_cast<float4 *>(&accx[o]) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                *reinterpret_cast<float4 *>(&accy[o]) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            } else {
-                if (cv.x < 0x10000u) { accx[o] = 0.0f; accy[o] = 0.0f; }
-                if (cv.y < 0x10000u) { accx[o + 1] = 0.0f; accy[o + 1] = 0.0f; }
-                if (cv.z < 0x10000u) { accx[o + 2] = 0.0f; accy[o + 2] = 0.0f; }
-                if (cv.w < 0x10000u) { accx[o + 3] = 0.0f; accy[o + 3] = 0.0f; }
-            }
+            *reinterpret_cast<uint4 *>(&tp[row * GM_TILE + c4]) =
+                *reinterpret_cast<const uint4 *>(&cnt[row * GM_STRIDE + c4]);
         }
+        if (tid == 0) pstamp[ty * g.tiles_x + tx] = cur_step;
         __syncthreads();
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) nfree += __shfl_xor(nfree, off, 64);
-    __shared__ long long s_free[GM_THREADS / 64];
-    if ((tid & 63) == 0) s_free[tid >> 6] = nfree;
-    __syncthreads();
-    if (tid == 0) {
-        long long f = 0;
-        for (int w = 0; w < GM_THREADS / 64; ++w) f += s_free[w];
-        st.free_updates = f;
-    }
+    if ((tid & 63) == 0 && nfree) atomicAdd(reinterpret_cast<unsigned long long *>(&st.free_updates), (unsigned long long)nfree);
 }
 
 // GMapping::PublishMap conversion (gmapping.cc:141-159): -1 unvisited, 100 if n/visits > thresh, 0
-__global__ void gm_publish_kernel(const int *__restrict__ pm, GmGeom g, GmState st, int8_t *__restrict__ out)
+__global__ void gm_publish_kernel(const unsigned *__restrict__ pm, const int *__restrict__ pstamp, GmGeom g, int step,
+                                  int8_t *__restrict__ out)
 {
     const size_t total = (size_t)g.sx * g.sy;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         const int x = (int)(i % g.sx), y = (int)(i / g.sx);
-        const int tx = x / GM_TILE, ty = y / GM_TILE_H;
+        const int t = (y / GM_TILE_H) * g.tiles_x + x / GM_TILE;
         int vis = 0, nn = 0;
-        if (tx >= st.tx0 && tx <= st.tx1 && ty >= st.ty0 && ty <= st.ty1) {
-            const int *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
-            const int c = (y % GM_TILE_H) * GM_TILE + (x % GM_TILE);
-            vis = tp[c];
-            nn = tp[GM_TILE_CELLS + c];
+        if (step > 0 && pstamp[t] == step) {
+            const unsigned cv = pm[(size_t)t * GM_TILE_BLOCK_WORDS + (y % GM_TILE_H) * GM_TILE + (x % GM_TILE)];
+            vis = (int)(cv & 0xFFFFu);
+            nn = (int)(cv >> 16);
         }
         const double occ = vis ? (double)nn * 1 / (double)vis : -1;
         out[i] = occ < 0 ? (int8_t)-1 : (occ > g.occ_thresh ? (int8_t)100 : (int8_t)0);

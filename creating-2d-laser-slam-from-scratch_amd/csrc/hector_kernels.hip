@@ -434,6 +434,29 @@ __device__ __forceinline__ unsigned make_ray(const LevelGeom &g, const RayFrame 
 //   step i in [0, da]:  a(i) = a0 + sa*i,  b(i) = b0 + sb*q(i),  q(i) = floor((e0 + i*db) / da),
 // e0 = da/2 (error_b start, :254/:260).  The incremental error walk keeps error in [0, da), so this
 // is exactly the cell sequence of the reference; steps 0..da-1 are freed, step da is the end cell.
+#ifndef S2D_FAST_UDIV
+#define S2D_FAST_UDIV 1
+#endif
+// n / d for n < 2^31, 1 <= d < 2^16: a float reciprocal estimate (relative error < 2^-22) and one
+// correction step each way -- ~8 instructions instead of the ~25 of the integer division sequence.
+// Exact whenever the quotient is < 2^16, which covers every step index (<= 32767) it is compared
+// with; a larger quotient stays > 2^15 and only ever means "beyond the walk".
+__device__ __forceinline__ unsigned udiv_small(unsigned n, unsigned d)
+{
+#if S2D_FAST_UDIV
+    unsigned q = (unsigned)((float)n * __builtin_amdgcn_rcpf((float)d));
+    int r = (int)(n - q * d);
+    if (r < 0) {
+        --q;
+        r += (int)d;
+    }
+    if (r >= (int)d) ++q;
+    return q;
+#else
+    return n / d;
+#endif
+}
+
 struct RayWalk {
     int a0, b0, sa, sb, da, db, e0;
     bool x_major;
@@ -483,11 +506,12 @@ __device__ __forceinline__ bool walk_range(const RayWalk &w, int A0, int A1, int
         if (qlo > 0) return false;  // q(i) == 0 for every step
         return true;
     }
-    if (qlo > 0) {
-        int t = (qlo * w.da - w.e0 + w.db - 1) / w.db;
+    if (qlo > 0) {  // numerator > 0: qlo * da - e0 >= da - da / 2
+        int t = (int)udiv_small((unsigned)(qlo * w.da - w.e0 + w.db - 1), (unsigned)w.db);
         if (t > lo) lo = t;
     }
-    int t2 = ((qhi + 1) * w.da - w.e0 - 1) / w.db;
+    // numerator >= 0: (qhi + 1) * da - e0 - 1 >= da - da / 2 - 1
+    int t2 = (int)udiv_small((unsigned)((qhi + 1) * w.da - w.e0 - 1), (unsigned)w.db);
     if (t2 < hi) hi = t2;
     return lo <= hi;
 }
@@ -670,6 +694,24 @@ hs_bin_kernel(FleetGeom geom, StreamState *__restrict__ state, const float2 *__r
             __syncthreads();
             const unsigned seg_base = s_base[0], item_base = s_base[1];
             whole = seg_base == 0xFFFFFFFFu;
+            if (whole) {
+                // the item slots reserved above are read by hs_tile_kernel (it walks every slot below
+                // item_used): fill the in-capacity ones with empty items (no segment, no row)
+                for (int k = tid; k < ne_total; k += BIN_THREADS) {
+                    const unsigned idx = item_base + (unsigned)k;
+                    if (idx >= item_cap) break;
+                    WorkItem it;
+                    it.s = s;
+                    it.lvl_kind = lvl | (ITEM_TILE << 8);
+                    it.tile_xy = (unsigned)tx0 | ((unsigned)ty0 << 16);
+                    it.begin_xy = begin_xy;
+                    it.seg_begin = 0;
+                    it.seg_count = 0;
+                    it.mark_base = (unsigned)st.mark_base;
+                    it.n = 0;
+                    items[idx] = it;
+                }
+            }
             if (!whole) {
                 // offsets + work items for this thread's chunk of tiles; s_off becomes the fill cursor
                 for (int t = t0; t < t1; ++t) {
@@ -988,9 +1030,17 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
 #define S2D_APPLY_UPD_LOAD 1  // 1: updateIndex quads loaded + stored whole; 0: per-cell masked stores
 #endif
 constexpr int UPD_STRIDE = S2D_UPD_STRIDE;            // LDS words per tile row (16-B rows, no 64-stride conflicts)
-constexpr int UPD_TILE_WORDS = TILE_H * UPD_STRIDE;   // one LDS mark array
+#ifndef S2D_UPD_TH
+#define S2D_UPD_TH 32
+#endif
+#ifndef S2D_UPD_MINB
+#define S2D_UPD_MINB 1  // __launch_bounds__ min workgroups per CU (caps VGPRs)
+#endif
+constexpr int UPD_TH = S2D_UPD_TH;                    // LDS tile height (a multiple of the storage TILE_H)
+static_assert(UPD_TH % TILE_H == 0, "an LDS tile covers whole storage tiles");
+constexpr int UPD_TILE_WORDS = UPD_TH * UPD_STRIDE;   // one LDS mark array
 static_assert(UPD_STRIDE % 4 == 0 && UPD_STRIDE >= TILE, "quad-aligned LDS rows");
-constexpr int UPD_QUADS = TILE_CELLS / 4 / UPD_THREADS;  // apply quads per thread per tile
+constexpr int UPD_QUADS = TILE * UPD_TH / 4 / UPD_THREADS;  // apply quads per thread per tile
 
 // bresenhamCellFree / bresenhamCellOcc outcome of one scan for one cell (h, f: first hitting /
 // freeing beam, W_NONE if none): GridMapLogOddsFunctions (GridMapLogOdds.h:108-129)
@@ -1011,6 +1061,14 @@ __device__ __forceinline__ int apply_cell(float &l, int &u, unsigned h, unsigned
     return 1;
 }
 
+// word offset of LDS-tile row `row` inside the level's tiled storage, relative to the LDS tile's
+// first storage tile (rows past TILE_H continue in the storage tile below)
+__device__ __forceinline__ int upd_off(int row, int tiles_x)
+{
+    if constexpr (UPD_TH == TILE_H) return row * TILE;
+    return (row / TILE_H) * tiles_x * TILE_BLOCK_WORDS + (row % TILE_H) * TILE;
+}
+
 __device__ __forceinline__ bool quad_marked(const uint4 &h, const uint4 &f)
 {
     return ((h.x & f.x) & (h.y & f.y) & (h.z & f.z) & (h.w & f.w)) != W_NONE;
@@ -1018,7 +1076,7 @@ __device__ __forceinline__ bool quad_marked(const uint4 &h, const uint4 &f)
 
 // Grid: for level l, upd_parts[l] x count blocks (level-major, then part, then stream); part p of a
 // level draws the tiles t = p, p + parts, ... of the scan's tile box (t row-major over the box).
-__global__ void __launch_bounds__(UPD_THREADS)
+__global__ void __launch_bounds__(UPD_THREADS, S2D_UPD_MINB)
 hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restrict__ state,
                  const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points)
 {
@@ -1043,6 +1101,10 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     const int tid = threadIdx.x;
     float *lvw = cells + (size_t)s * geom.stream_words + g.word_offset;
 
+#ifdef S2D_STAMPS
+    unsigned long long t_a = 0, t_b = 0, t_c = 0, t_d = 0, c_setup = 0, c_raster = 0, c_apply = 0, n_tiles = 0;
+    S2D_STAMP(t_a);
+#endif
     const RayFrame fr = ray_frame(g, st);
     const int x0 = fr.bxi, y0 = fr.byi;
     if (tid == 0) {
@@ -1092,18 +1154,22 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         atomicAdd(&state[s].tot_rays, R);
     }
     if (!__syncthreads_or(R != 0)) return;  // no ray drawn on this level
-    const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / TILE_H;
-    const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / TILE_H;
+    const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / UPD_TH;
+    const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / UPD_TH;
     const int mark_free = st.mark_base + 1;  // currMarkFreeIndex (:120)
     const int mark_occ = st.mark_base + 2;   // currMarkOccIndex  (:121)
     const float lf = geom.lf, lo = geom.lo;
     unsigned touched = 0;
 
     const int ntx = tx1 - tx0 + 1, ntiles = ntx * (ty1 - ty0 + 1);
+#ifdef S2D_STAMPS
+    S2D_STAMP(t_b);
+    c_setup = t_b - t_a;
+#endif
     for (int t = part; t < ntiles; t += parts) {
         const int ty = ty0 + t / ntx, tx = tx0 + t % ntx;
-        const int X0 = tx * TILE, Y0 = ty * TILE_H;
-        const int X1 = X0 + TILE, Y1 = Y0 + TILE_H;
+        const int X0 = tx * TILE, Y0 = ty * UPD_TH;
+        const int X1 = X0 + TILE, Y1 = Y0 + UPD_TH;
         for (int k = tid; k < 2 * UPD_TILE_WORDS / 4; k += UPD_THREADS)
             reinterpret_cast<uint4 *>(smem)[k] = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
         __syncthreads();
@@ -1132,7 +1198,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             if (lo_i > hi_i) continue;
             any = true;
             const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
-            const int q = (int)(num / (unsigned)w.da);
+            const int q = (int)udiv_small(num, (unsigned)w.da);
             int err = (int)(num - (unsigned)q * (unsigned)w.da);
             // local LDS index of step lo_i and its increments along the major / minor axis
             const int la = w.x_major ? 1 : UPD_STRIDE;
@@ -1151,11 +1217,18 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 }
             }
         }
-        if (!__syncthreads_or(any)) continue;
+        const bool tile_any = __syncthreads_or(any);
+#ifdef S2D_STAMPS
+        S2D_STAMP(t_c);
+        c_raster += t_c - t_b;
+        t_b = t_c;
+#endif
+        if (!tile_any) continue;
         // apply: thread owns quads q = tid + j * 256 (16 quads per 64-cell row): 16-B LDS reads,
         // 16-B global loads / stores of both planes for every quad holding a mark.  Cells outside
         // the map (padding of edge tiles) never carry marks and are rewritten unchanged.
-        float *tl = lvw + (size_t)(tx + ty * g.tiles_x) * TILE_BLOCK_WORDS;
+        // quad qi: LDS row qi / 16, storage tile (tx, (Y0 + row) / TILE_H), storage row (Y0 + row) % TILE_H
+        float *tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
         int *tu = reinterpret_cast<int *>(tl + TILE_CELLS);
         uint4 qh[UPD_QUADS], qf[UPD_QUADS];
         float4 ql[UPD_QUADS];
@@ -1169,9 +1242,9 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             qf[j] = *reinterpret_cast<const uint4 *>(&first_free[row * UPD_STRIDE + c4]);
             qm[j] = quad_marked(qh[j], qf[j]);
             if (qm[j]) {
-                ql[j] = *reinterpret_cast<const float4 *>(&tl[row * TILE + c4]);
+                ql[j] = *reinterpret_cast<const float4 *>(&tl[upd_off(row, g.tiles_x) + c4]);
 #if S2D_APPLY_UPD_LOAD
-                qu[j] = *reinterpret_cast<const int4 *>(&tu[row * TILE + c4]);
+                qu[j] = *reinterpret_cast<const int4 *>(&tu[upd_off(row, g.tiles_x) + c4]);
 #endif
             }
         }
@@ -1185,8 +1258,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             touched += apply_cell(ql[j].y, qu[j].y, qh[j].y, qf[j].y, lf, lo, mark_free, mark_occ);
             touched += apply_cell(ql[j].z, qu[j].z, qh[j].z, qf[j].z, lf, lo, mark_free, mark_occ);
             touched += apply_cell(ql[j].w, qu[j].w, qh[j].w, qf[j].w, lf, lo, mark_free, mark_occ);
-            *reinterpret_cast<float4 *>(&tl[row * TILE + c4]) = ql[j];
-            *reinterpret_cast<int4 *>(&tu[row * TILE + c4]) = qu[j];
+            *reinterpret_cast<float4 *>(&tl[upd_off(row, g.tiles_x) + c4]) = ql[j];
+            *reinterpret_cast<int4 *>(&tu[upd_off(row, g.tiles_x) + c4]) = qu[j];
 #else
             int u[4];
             const int t0 = apply_cell(ql[j].x, u[0], qh[j].x, qf[j].x, lf, lo, mark_free, mark_occ);
@@ -1194,18 +1267,33 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             const int t2 = apply_cell(ql[j].z, u[2], qh[j].z, qf[j].z, lf, lo, mark_free, mark_occ);
             const int t3 = apply_cell(ql[j].w, u[3], qh[j].w, qf[j].w, lf, lo, mark_free, mark_occ);
             touched += t0 + t1 + t2 + t3;
-            *reinterpret_cast<float4 *>(&tl[row * TILE + c4]) = ql[j];
-            if (t0) tu[row * TILE + c4 + 0] = u[0];
-            if (t1) tu[row * TILE + c4 + 1] = u[1];
-            if (t2) tu[row * TILE + c4 + 2] = u[2];
-            if (t3) tu[row * TILE + c4 + 3] = u[3];
+            const int o = upd_off(row, g.tiles_x) + c4;
+            *reinterpret_cast<float4 *>(&tl[o]) = ql[j];
+            if (t0) tu[o + 0] = u[0];
+            if (t1) tu[o + 1] = u[1];
+            if (t2) tu[o + 2] = u[2];
+            if (t3) tu[o + 3] = u[3];
 #endif
         }
         __syncthreads();
+#ifdef S2D_STAMPS
+        S2D_STAMP(t_d);
+        c_apply += t_d - t_b;
+        t_b = t_d;
+        ++n_tiles;
+#endif
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);
     if ((tid & 63) == 0 && touched) atomicAdd(&state[s].tot_touched, (unsigned long long)touched);
+#ifdef S2D_STAMPS
+    if (tid == 0) {
+        atomicAdd(&g_stamps[0], c_setup);
+        atomicAdd(&g_stamps[1], c_raster);
+        atomicAdd(&g_stamps[2], c_apply);
+        atomicAdd(&g_stamps[3], n_tiles);
+    }
+#endif
 }
 
 

@@ -1,0 +1,28 @@
+"""Diagnostic: hs_update_kernel phase shares from s_memtime stamps (SLAM2D_LIB=.../libslam2d_stamps.so)."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "creating-2d-laser-slam-from-scratch_amd", "python"))
+import numpy as np
+import torch
+from slam2d import synth
+from slam2d.hector import HectorFleet
+
+B = int(os.environ.get("B", "1024")); T = 8
+S = synth.make_streams(B, T)
+pts = torch.from_numpy(np.ascontiguousarray(S.points.transpose(1, 0, 2, 3))).cuda()
+cnt = torch.from_numpy(np.ascontiguousarray(S.counts.T.astype(np.int32))).cuda()
+f = HectorFleet(B, 0.05, 2048, (0.5, 0.5), 3, max_points=1081)
+f.set_update_factors(0.4, 0.9); f.set_thresholds(-1, -1)
+sb = pts.shape[1] * pts.shape[2] * 8
+for t in range(T):
+    if t == T - 1:
+        f.queue_stats(reset_stamps=True)
+        f.set_timing(True)
+    f.step_device(pts.data_ptr() + t * sb, pts.shape[2], cnt[t].data_ptr())
+torch.cuda.synchronize()
+q = f.queue_stats(); kt = f.kernel_times()
+print("kernel ms:", kt)
+tot = q["cyc_setup"] + q["cyc_raster"] + q["cyc_apply"]
+blocks = B * 3
+print("per block: setup %.0f raster %.0f apply %.0f cycles; nonempty tiles/block %.1f" % (
+    q["cyc_setup"] / blocks, q["cyc_raster"] / blocks, q["cyc_apply"] / blocks, q["tiles"] / blocks))
+print("shares: setup %.3f raster %.3f apply %.3f" % (q["cyc_setup"] / tot, q["cyc_raster"] / tot, q["cyc_apply"] / tot))

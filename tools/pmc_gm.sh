@@ -1,0 +1,24 @@
+#!/bin/bash
+# SQ counter passes over the GMapping bench: tools/pmc_gm.sh <tag>
+TAG=${1:-x}; shift
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/pmcgm_$TAG; mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd /tmp
+i=0
+for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_ADDR_CONFLICT"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set -d "$OUT/p$i" -o run --output-format csv -- python3 "$ROOT/bench.py" --config gmapping --no-cpu-baseline --steps 5 --warmup 2 "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; }
+done
+python3 - "$OUT" <<'PY'
+import csv, glob, sys, collections
+agg = collections.defaultdict(float); cnt = collections.Counter()
+for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].split("(")[0].replace("s2d::", "")
+        agg[(k, r["Counter_Name"])] += float(r["Counter_Value"]); cnt[(k, r["Counter_Name"])] += 1
+for (k, c), v in sorted(agg.items()):
+    if k.startswith("gm_"): print(f"{k:24s} {c:24s} {v/ max(cnt[(k,c)],1):18.0f} (per dispatch avg over {cnt[(k,c)]})")
+PY

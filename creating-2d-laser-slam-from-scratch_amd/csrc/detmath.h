@@ -179,4 +179,67 @@ SDM_FN float sdm_expf(float x)
     return (x != x) ? x : ((x > 88.72284f) ? HUGE_VALF : ((x < -103.97909f) ? 0.0f : res));
 }
 
+
+/* atan / atan2 in double (PL-ICP possible_interval, CSM icp_corr_dumb.c): |x| > 1 -> pi/2 - atan(1/x);
+ * t > tan(pi/12) -> pi/6 + atan((t*sqrt3 - 1)/(sqrt3 + t)); Taylor series to u^29 on |u| <= 0.268
+ * (truncation < 1e-18).  Same op sequence on host and device. */
+#define SDM_AT0 1.0
+#define SDM_AT1 -0.3333333333333333
+#define SDM_AT2 0.2
+#define SDM_AT3 -0.14285714285714285
+#define SDM_AT4 0.1111111111111111
+#define SDM_AT5 -0.09090909090909091
+#define SDM_AT6 0.07692307692307693
+#define SDM_AT7 -0.06666666666666667
+#define SDM_AT8 0.058823529411764705
+#define SDM_AT9 -0.05263157894736842
+#define SDM_AT10 0.047619047619047616
+#define SDM_AT11 -0.043478260869565216
+#define SDM_AT12 0.04
+#define SDM_AT13 -0.037037037037037035
+#define SDM_AT14 0.034482758620689655
+#define SDM_SQRT3 1.7320508075688772
+#define SDM_PI 3.141592653589793
+#define SDM_PI_2 1.5707963267948966
+#define SDM_PI_6 0.5235987755982988
+#define SDM_TAN_PI_12 0.2679491924311227
+SDM_FN double sdm_atan(double x)
+{
+    if (x != x) return x;
+    const double ax = fabs(x);
+    const int inv = ax > 1.0;
+    const double t = inv ? 1.0 / ax : ax;
+    const int red = t > SDM_TAN_PI_12;
+    const double u = red ? (t * SDM_SQRT3 - 1.0) / (SDM_SQRT3 + t) : t;
+    const double z = u * u;
+    double p = SDM_AT14;
+    p = SDM_AT13 + z * p;
+    p = SDM_AT12 + z * p;
+    p = SDM_AT11 + z * p;
+    p = SDM_AT10 + z * p;
+    p = SDM_AT9 + z * p;
+    p = SDM_AT8 + z * p;
+    p = SDM_AT7 + z * p;
+    p = SDM_AT6 + z * p;
+    p = SDM_AT5 + z * p;
+    p = SDM_AT4 + z * p;
+    p = SDM_AT3 + z * p;
+    p = SDM_AT2 + z * p;
+    p = SDM_AT1 + z * p;
+    p = SDM_AT0 + z * p;
+    double r = u * p;
+    if (red) r = SDM_PI_6 + r;
+    if (inv) r = SDM_PI_2 - r;
+    return x < 0.0 ? -r : r;
+}
+SDM_FN double sdm_atan2(double y, double x)
+{
+    if (x != x || y != y) return x + y;
+    if (x > 0.0) return sdm_atan(y / x);
+    if (x < 0.0) return y >= 0.0 ? sdm_atan(y / x) + SDM_PI : sdm_atan(y / x) - SDM_PI;
+    if (y > 0.0) return SDM_PI_2;
+    if (y < 0.0) return -SDM_PI_2;
+    return 0.0;
+}
+
 #endif

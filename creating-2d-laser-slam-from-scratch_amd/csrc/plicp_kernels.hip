@@ -1,0 +1,459 @@
+// plicp_kernels.hip -- MI355X kernel of the PL-ICP scan-matching path (lesson3 front-end).
+//
+//   pl_icp_kernel   one 256-thread workgroup per scan pair: the whole point-to-line ICP loop of CSM's
+//                   sm_icp as lesson3 configures it (lesson3/src/plicp_odometry.cc:58-186, :391), in
+//                   double precision.  Per iteration:
+//                     correspondences  every thread owns rays i = tid + 256 k; exact closest valid
+//                                      reference point inside CSM's polar search interval (reference
+//                                      points resident in LDS), j2 = closer valid neighbour;
+//                     trimming         the two order statistics of the point-to-segment errors by an
+//                                      8-pass radix select on the errors' bit patterns (LDS histograms);
+//                     doubles          per-reference minimum dist^2 by LDS 64-bit atomicMin on the bits;
+//                     estimate         the 14 point-to-line GPC sums (64-lane xor butterfly, then the
+//                                      4 waves), the constrained 4x4 solve by every thread (bisection on
+//                                      the Lagrange multiplier), oscillation hash, convergence test.
+// The CPU checker oracle/plicp_oracle.c evaluates the same op sequence (-ffp-contract=off here and
+// there), so results agree bit for bit; CSM itself is absent (parity unpinned).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/slam2d/plicp.h"
+#include "detmath.h"
+
+namespace s2d {
+
+constexpr int PL_THREADS = 256;
+constexpr int PL_RPT = 8;                       // rays per thread: max_rays <= 2048
+constexpr int PL_MAX_RAYS = PL_THREADS * PL_RPT;
+constexpr int PL_MAX_IT = 64;
+
+__device__ __forceinline__ double pl_dist_to_segment(double ax, double ay, double bx, double by, double x, double y)
+{
+    const double t0 = ax - bx, t1 = ay - by;
+    const double one_on_r = 1.0 / sqrt(t0 * t0 + t1 * t1);
+    const double nx = t1 * one_on_r, ny = -t0 * one_on_r;
+    const double rho = nx * ax + ny * ay;
+    const double lx = (nx * rho + ny * ny * x) - nx * ny * y;
+    const double ly = (ny * rho - nx * ny * x) + nx * nx * y;
+    double qx, qy;
+    if ((lx - ax) * (lx - bx) + (ly - ay) * (ly - by) < 0.0) {
+        qx = lx;
+        qy = ly;
+    } else {
+        const double da = (ax - x) * (ax - x) + (ay - y) * (ay - y);
+        const double db = (bx - x) * (bx - x) + (by - y) * (by - y);
+        if (da < db) {
+            qx = ax;
+            qy = ay;
+        } else {
+            qx = bx;
+            qy = by;
+        }
+    }
+    return sqrt((qx - x) * (qx - x) + (qy - y) * (qy - y));
+}
+
+// possible_interval (CSM icp_corr_dumb.c)
+__device__ __forceinline__ void pl_interval(const pl_params &p, double wx, double wy, int n, double min_theta,
+                                            double max_theta, int &from, int &to)
+{
+    const double angle_res = (max_theta - min_theta) / n;
+    const double norm = sqrt(wx * wx + wy * wy);
+    const double delta = fabs(p.max_angular_correction_deg * (SDM_PI / 180.0)) + fabs(sdm_atan(p.max_linear_correction / norm));
+    const int range = (int)ceil(delta / angle_res);
+    double start_theta = sdm_atan2(wy, wx);
+    if (start_theta < min_theta) start_theta += 2.0 * SDM_PI;
+    if (start_theta > max_theta) start_theta -= 2.0 * SDM_PI;
+    const int start_cell = (int)((start_theta - min_theta) / (max_theta - min_theta) * n);
+    const int f = start_cell - range, t = start_cell + range;
+    from = f < 0 ? 0 : (f > n - 1 ? n - 1 : f);
+    to = t < 0 ? 0 : (t > n - 1 ? n - 1 : t);
+}
+
+// the 14 GPC terms of one correspondence (upper triangle of M_k^T C M_k, then g = -2 M_k^T C q)
+__device__ __forceinline__ void pl_terms(double px, double py, double qx, double qy, double c00, double c01,
+                                         double c11, double *o)
+{
+    o[0] = c00;
+    o[1] = c01;
+    o[2] = c00 * px + c01 * py;
+    o[3] = -c00 * py + c01 * px;
+    o[4] = c11;
+    o[5] = c01 * px + c11 * py;
+    o[6] = -c01 * py + c11 * px;
+    o[7] = (c00 * px * px + 2.0 * c01 * px * py) + c11 * py * py;
+    o[8] = ((-c00 * px * py + c01 * px * px) - c01 * py * py) + c11 * px * py;
+    o[9] = (c00 * py * py - 2.0 * c01 * px * py) + c11 * px * px;
+    const double a0 = c00 * qx + c01 * qy, a1 = c01 * qx + c11 * qy;
+    o[10] = -2.0 * a0;
+    o[11] = -2.0 * a1;
+    o[12] = -2.0 * (px * a0 + py * a1);
+    o[13] = -2.0 * (-py * a0 + px * a1);
+}
+
+// constrained point-to-line solve (the role of CSM's gpc_solve); false if degenerate
+__device__ __forceinline__ bool pl_gpc_solve(const double *m, double *x)
+{
+    const double m00 = m[0], m01 = m[1], m02 = m[2], m03 = m[3], m11 = m[4], m12 = m[5], m13 = m[6];
+    const double m22 = m[7], m23 = m[8], m33 = m[9];
+    const double g0 = m[10], g1 = m[11], g2 = m[12], g3 = m[13];
+    const double detA = m00 * m11 - m01 * m01;
+    if (!(detA > 0.0)) return false;
+    const double ia00 = m11 / detA, ia01 = -m01 / detA, ia11 = m00 / detA;
+    const double ab00 = ia00 * m02 + ia01 * m12, ab01 = ia00 * m03 + ia01 * m13;
+    const double ab10 = ia01 * m02 + ia11 * m12, ab11 = ia01 * m03 + ia11 * m13;
+    const double s00 = m22 - (m02 * ab00 + m12 * ab10);
+    const double s01 = m23 - (m02 * ab01 + m12 * ab11);
+    const double s11 = m33 - (m03 * ab01 + m13 * ab11);
+    const double agt0 = ia00 * g0 + ia01 * g1, agt1 = ia01 * g0 + ia11 * g1;
+    const double h0 = -0.5 * g2 + 0.5 * (m02 * agt0 + m12 * agt1);
+    const double h1 = -0.5 * g3 + 0.5 * (m03 * agt0 + m13 * agt1);
+    const double hn = sqrt(h0 * h0 + h1 * h1);
+    if (!(hn > 0.0)) return false;
+    const double mid = 0.5 * (s00 + s11);
+    const double rad = sqrt(0.25 * (s00 - s11) * (s00 - s11) + s01 * s01);
+    const double lmin = mid - rad;
+    double lo = -lmin, hi = -lmin + hn;
+    for (int it = 0; it < 200; ++it) {
+        const double l = 0.5 * (lo + hi);
+        const double a = s00 + l, d = s11 + l;
+        const double det = a * d - s01 * s01;
+        const double r0 = (d * h0 - s01 * h1) / det, r1 = (a * h1 - s01 * h0) / det;
+        if (r0 * r0 + r1 * r1 > 1.0) lo = l;
+        else hi = l;
+    }
+    const double l = 0.5 * (lo + hi);
+    const double a = s00 + l, d = s11 + l;
+    const double det = a * d - s01 * s01;
+    const double r0 = (d * h0 - s01 * h1) / det, r1 = (a * h1 - s01 * h0) / det;
+    const double br0 = (m02 * r0 + m03 * r1) + 0.5 * g0, br1 = (m12 * r0 + m13 * r1) + 0.5 * g1;
+    x[0] = -(ia00 * br0 + ia01 * br1);
+    x[1] = -(ia01 * br0 + ia11 * br1);
+    x[2] = sdm_atan2(r1, r0);
+    return isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
+}
+
+__device__ __forceinline__ unsigned pl_mix(unsigned x)
+{
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ double pl_angle_diff(double a, double b)
+{
+    double d = a - b;
+    while (d > SDM_PI) d -= 2.0 * SDM_PI;
+    while (d <= -SDM_PI) d += 2.0 * SDM_PI;
+    return d;
+}
+
+// block-wide sums (xor butterfly inside each wave, then ((w0 + w2) + (w1 + w3)) -- the oracle's
+// reduce_threads = 256 order)
+template <int K>
+__device__ __forceinline__ void pl_block_sum(double *v, double (*red)[16])
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = v[k] + __shfl_xor(v[k], off, 64);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[w][k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = (red[0][k] + red[2][k]) + (red[1][k] + red[3][k]);
+    __syncthreads();
+}
+
+__device__ __forceinline__ int pl_block_sum_int(int v, int *sred)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const int r = (sred[0] + sred[1]) + (sred[2] + sred[3]);
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(PL_THREADS)
+pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const double *__restrict__ ref_r,
+              const double *__restrict__ sens_r, const double *__restrict__ first_guess, pl_result *__restrict__ out)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char pl_smem[];
+    double2 *rpt = reinterpret_cast<double2 *>(pl_smem);                          // reference points [n]
+    unsigned long long *best_j = reinterpret_cast<unsigned long long *>(rpt + n);   // [n]
+    int16_t *rup = reinterpret_cast<int16_t *>(best_j + n);                         // next valid above [n]
+    int16_t *rdn = rup + n;                                                         // next valid below [n]
+    __shared__ double red[4][16];
+    __shared__ int sred[4];
+    __shared__ unsigned hist[512];
+    __shared__ unsigned long long s_pref[2];
+    __shared__ int s_rank[2];
+    __shared__ unsigned s_hash[PL_MAX_IT];
+
+    const int pair = blockIdx.x;
+    const int tid = threadIdx.x;
+    const double *rr = ref_r + (size_t)pair * n;
+    const double *sr = sens_r + (size_t)pair * n;
+
+    // ---- LDP -> cartesian (LaserScanToLDP :285-322, ld_compute_cartesian); valid <=> reading > 0.
+    // Invalid reference rays are parked at 1e300: their squared distance overflows to +inf, so the
+    // `dist > max_correspondence_dist^2` test skips them exactly like ld_valid_ray does.
+    for (int i = tid; i < n; i += PL_THREADS) {
+        const double r = rr[i];
+        const double th = angle_min + i * angle_inc;
+        rpt[i] = r > 0.0 ? make_double2(r * sdm_cos(th), r * sdm_sin(th)) : make_double2(1e300, 1e300);
+    }
+    double spx[PL_RPT], spy[PL_RPT];
+    bool sval[PL_RPT];
+#pragma unroll
+    for (int k = 0; k < PL_RPT; ++k) {
+        const int i = tid + k * PL_THREADS;
+        sval[k] = false;
+        spx[k] = spy[k] = 0.0;
+        if (i < n) {
+            const double r = sr[i];
+            const double th = angle_min + i * angle_inc;
+            sval[k] = r > 0.0;
+            if (sval[k]) {
+                spx[k] = r * sdm_cos(th);
+                spy[k] = r * sdm_sin(th);
+            }
+        }
+    }
+    // next valid neighbours of every reference ray (wave 0 scans serially in both directions)
+    if (tid == 0) {
+        int last = -1;
+        for (int i = 0; i < n; ++i) {
+            rdn[i] = (int16_t)last;
+            if (rr[i] > 0.0) last = i;
+        }
+    } else if (tid == 64) {
+        int last = -1;
+        for (int i = n - 1; i >= 0; --i) {
+            rup[i] = (int16_t)last;
+            if (rr[i] > 0.0) last = i;
+        }
+    }
+    __syncthreads();
+
+    const double min_theta = angle_min, max_theta = angle_min + (n - 1) * angle_inc;
+    const double maxd2 = p.max_correspondence_dist * p.max_correspondence_dist;
+    const int max_it = p.max_iterations < PL_MAX_IT ? p.max_iterations : PL_MAX_IT;
+    double x_old[3], x_new[3];
+    if (first_guess) {
+        x_old[0] = first_guess[3 * pair];
+        x_old[1] = first_guess[3 * pair + 1];
+        x_old[2] = first_guess[3 * pair + 2];
+    } else {
+        x_old[0] = x_old[1] = x_old[2] = 0.0;
+    }
+    x_new[0] = x_old[0];
+    x_new[1] = x_old[1];
+    x_new[2] = x_old[2];
+    bool all_ok = true;
+    int it = 0, nvalid = 0;
+    double total_error = 0.0;
+    int j1[PL_RPT], j2[PL_RPT];
+    bool ok[PL_RPT];
+    double d2[PL_RPT], e[PL_RPT];
+
+    for (it = 0; it < max_it; ++it) {
+        const double c = sdm_cos(x_old[2]), s = sdm_sin(x_old[2]);
+        int ncorr = 0;
+#pragma unroll
+        for (int k = 0; k < PL_RPT; ++k) {
+            ok[k] = false;
+            j1[k] = j2[k] = -1;
+            d2[k] = e[k] = 0.0;
+            const int i = tid + k * PL_THREADS;
+            if (i >= n || !sval[k]) continue;
+            const double wx = (c * spx[k] - s * spy[k]) + x_old[0];   // ld_compute_world_coords
+            const double wy = (s * spx[k] + c * spy[k]) + x_old[1];
+            int from, to;
+            pl_interval(p, wx, wy, n, min_theta, max_theta, from, to);
+            int b1 = -1;
+            double best = 0.0;
+            for (int j = from; j <= to; ++j) {
+                const double2 q = rpt[j];
+                const double dx = wx - q.x, dy = wy - q.y;
+                const double dist = dx * dx + dy * dy;
+                if (dist > maxd2) continue;
+                if (b1 == -1 || dist < best) {
+                    b1 = j;
+                    best = dist;
+                }
+            }
+            if (b1 == -1 || b1 == 0 || b1 == n - 1) continue;   // no match / extrema
+            const int up = rup[b1], dn = rdn[b1];
+            if (up == -1 && dn == -1) continue;
+            int b2;
+            if (up == -1) b2 = dn;
+            else if (dn == -1) b2 = up;
+            else {
+                const double2 qu = rpt[up], qd = rpt[dn];
+                const double du = (wx - qu.x) * (wx - qu.x) + (wy - qu.y) * (wy - qu.y);
+                const double dd = (wx - qd.x) * (wx - qd.x) + (wy - qd.y) * (wy - qd.y);
+                b2 = du < dd ? up : dn;
+            }
+            j1[k] = b1;
+            j2[k] = b2;
+            d2[k] = best;
+            ok[k] = true;
+            ++ncorr;
+            const double2 q1 = rpt[b1], q2 = rpt[b2];
+            e[k] = pl_dist_to_segment(q1.x, q1.y, q2.x, q2.y, wx, wy);
+        }
+        ncorr = pl_block_sum_int(ncorr, sred);
+        if (ncorr < 0.05 * n) {
+            all_ok = false;
+            break;
+        }
+        // ---- kill_outliers_trim: two order statistics of the k errors (radix select on the bits)
+        const int kk = ncorr;
+        int order = (int)floor(kk * p.outliers_maxPerc);
+        order = order < 0 ? 0 : (order > kk - 1 ? kk - 1 : order);
+        int order2 = (int)floor(kk * p.outliers_adaptive_order);
+        order2 = order2 < 0 ? 0 : (order2 > kk - 1 ? kk - 1 : order2);
+        unsigned long long pref0 = 0, pref1 = 0;
+        int rank0 = order, rank1 = order2;
+        for (int shift = 56; shift >= 0; shift -= 8) {
+            for (int b = tid; b < 512; b += PL_THREADS) hist[b] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PL_RPT; ++k) {
+                if (!ok[k]) continue;
+                const unsigned long long key = (unsigned long long)__double_as_longlong(e[k]);
+                const unsigned d = (unsigned)(key >> shift) & 255u;
+                const bool m0 = shift == 56 || (key >> (shift + 8)) == (pref0 >> (shift + 8));
+                const bool m1 = shift == 56 || (key >> (shift + 8)) == (pref1 >> (shift + 8));
+                if (m0) atomicAdd(&hist[d], 1u);
+                if (m1) atomicAdd(&hist[256 + d], 1u);
+            }
+            __syncthreads();
+            if (tid == 0 || tid == 64) {
+                const int h = tid == 0 ? 0 : 1;
+                int r = h == 0 ? rank0 : rank1;
+                unsigned cum = 0;
+                int b = 0;
+                for (; b < 255; ++b) {
+                    const unsigned c2 = hist[256 * h + b];
+                    if (cum + c2 > (unsigned)r) break;
+                    cum += c2;
+                }
+                s_pref[h] = (h == 0 ? pref0 : pref1) | ((unsigned long long)b << shift);
+                s_rank[h] = r - (int)cum;
+            }
+            __syncthreads();
+            pref0 = s_pref[0];
+            pref1 = s_pref[1];
+            rank0 = s_rank[0];
+            rank1 = s_rank[1];
+            __syncthreads();
+        }
+        const double lim1 = __longlong_as_double((long long)pref0);
+        const double lim2 = p.outliers_adaptive_mult * __longlong_as_double((long long)pref1);
+        const double limit = lim1 < lim2 ? lim1 : lim2;
+        double err_sum[1] = {0.0};
+        int nv = 0;
+#pragma unroll
+        for (int k = 0; k < PL_RPT; ++k) {
+            if (!ok[k]) continue;
+            if (e[k] > limit) ok[k] = false;
+            else {
+                ++nv;
+                err_sum[0] = err_sum[0] + e[k];
+            }
+        }
+        nvalid = pl_block_sum_int(nv, sred);
+        pl_block_sum<1>(err_sum, red);
+        total_error = err_sum[0];
+        // ---- kill_outliers_double
+        if (p.outliers_remove_doubles) {
+            const unsigned long long init = (unsigned long long)__double_as_longlong(1000000.0);
+            for (int j = tid; j < n; j += PL_THREADS) best_j[j] = init;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PL_RPT; ++k)
+                if (ok[k]) atomicMin(&best_j[j1[k]], (unsigned long long)__double_as_longlong(d2[k]));
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PL_RPT; ++k)
+                if (ok[k] && d2[k] > 9.0 * __longlong_as_double((long long)best_j[j1[k]])) ok[k] = false;
+        }
+        // ---- compute_next_estimate: point-to-line GPC sums + constrained solve
+        double m[14];
+#pragma unroll
+        for (int q = 0; q < 14; ++q) m[q] = 0.0;
+        unsigned hsum = 0;
+#pragma unroll
+        for (int k = 0; k < PL_RPT; ++k) {
+            const int i = tid + k * PL_THREADS;
+            if (i < n) hsum += pl_mix((unsigned)i * 0x9E3779B9U ^ (ok[k] ? (unsigned)(j1[k] + 1000 * j2[k]) : 0xFFFFFFFFu));
+            if (!ok[k]) continue;
+            const double2 q1 = rpt[j1[k]], q2 = rpt[j2[k]];
+            double c00, c01, c11;
+            if (p.use_point_to_line_distance) {
+                const double dfx = q1.x - q2.x, dfy = q1.y - q2.y;
+                const double one_on_norm = 1.0 / sqrt(dfx * dfx + dfy * dfy);
+                const double nx = dfy * one_on_norm, ny = -dfx * one_on_norm;
+                c00 = nx * nx;
+                c01 = nx * ny;
+                c11 = ny * ny;
+            } else {
+                c00 = 1.0;
+                c01 = 0.0;
+                c11 = 1.0;
+            }
+            double t[14];
+            pl_terms(spx[k], spy[k], q1.x, q1.y, c00, c01, c11, t);
+#pragma unroll
+            for (int q = 0; q < 14; ++q) m[q] = m[q] + t[q];
+        }
+        pl_block_sum<14>(m, red);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) hsum += __shfl_xor(hsum, off, 64);
+        if ((tid & 63) == 0) sred[tid >> 6] = (int)hsum;
+        __syncthreads();
+        const unsigned hash = ((unsigned)sred[0] + (unsigned)sred[1] + (unsigned)sred[2] + (unsigned)sred[3]) & 0x7FFFFFFFu;
+        __syncthreads();
+        if (!pl_gpc_solve(m, x_new)) {
+            all_ok = false;
+            break;
+        }
+        const double co = sdm_cos(x_old[2]), so = sdm_sin(x_old[2]);
+        const double ddx = x_new[0] - x_old[0], ddy = x_new[1] - x_old[1];
+        const double dl0 = co * ddx + so * ddy, dl1 = -so * ddx + co * ddy, dl2 = pl_angle_diff(x_new[2], x_old[2]);
+        if (tid == 0) s_hash[it] = hash;
+        __syncthreads();
+        bool loop = false;
+        for (int a = 0; a < it; ++a)
+            if (s_hash[a] == hash) loop = true;
+        if (loop) break;
+        if (fabs(dl0) < p.epsilon_xy && fabs(dl1) < p.epsilon_xy && fabs(dl2) < p.epsilon_theta) break;
+        x_old[0] = x_new[0];
+        x_old[1] = x_new[1];
+        x_old[2] = x_new[2];
+    }
+    if (tid == 0) {
+        pl_result r;
+        r.x[0] = x_new[0];
+        r.x[1] = x_new[1];
+        r.x[2] = x_new[2];
+        r.error = total_error;
+        r.valid = all_ok ? 1 : 0;
+        r.iterations = it + (it < max_it ? 1 : 0);
+        r.nvalid = nvalid;
+        r.pad_ = 0;
+        out[pair] = r;
+    }
+}
+
+}  // namespace s2d

@@ -171,4 +171,67 @@ static inline float odm_expf(float x)
     return (x != x) ? x : ((x > 88.72284f) ? HUGE_VALF : ((x < -103.97909f) ? 0.0f : res));
 }
 
+
+/* atan / atan2 in double (PL-ICP possible_interval, CSM icp_corr_dumb.c): |x| > 1 -> pi/2 - atan(1/x);
+ * t > tan(pi/12) -> pi/6 + atan((t*sqrt3 - 1)/(sqrt3 + t)); Taylor series to u^29 on |u| <= 0.268
+ * (truncation < 1e-18).  Same op sequence on host and device. */
+#define ODM_AT0 1.0
+#define ODM_AT1 -0.3333333333333333
+#define ODM_AT2 0.2
+#define ODM_AT3 -0.14285714285714285
+#define ODM_AT4 0.1111111111111111
+#define ODM_AT5 -0.09090909090909091
+#define ODM_AT6 0.07692307692307693
+#define ODM_AT7 -0.06666666666666667
+#define ODM_AT8 0.058823529411764705
+#define ODM_AT9 -0.05263157894736842
+#define ODM_AT10 0.047619047619047616
+#define ODM_AT11 -0.043478260869565216
+#define ODM_AT12 0.04
+#define ODM_AT13 -0.037037037037037035
+#define ODM_AT14 0.034482758620689655
+#define ODM_SQRT3 1.7320508075688772
+#define ODM_PI 3.141592653589793
+#define ODM_PI_2 1.5707963267948966
+#define ODM_PI_6 0.5235987755982988
+#define ODM_TAN_PI_12 0.2679491924311227
+static inline double odm_atan(double x)
+{
+    if (x != x) return x;
+    const double ax = fabs(x);
+    const int inv = ax > 1.0;
+    const double t = inv ? 1.0 / ax : ax;
+    const int red = t > ODM_TAN_PI_12;
+    const double u = red ? (t * ODM_SQRT3 - 1.0) / (ODM_SQRT3 + t) : t;
+    const double z = u * u;
+    double p = ODM_AT14;
+    p = ODM_AT13 + z * p;
+    p = ODM_AT12 + z * p;
+    p = ODM_AT11 + z * p;
+    p = ODM_AT10 + z * p;
+    p = ODM_AT9 + z * p;
+    p = ODM_AT8 + z * p;
+    p = ODM_AT7 + z * p;
+    p = ODM_AT6 + z * p;
+    p = ODM_AT5 + z * p;
+    p = ODM_AT4 + z * p;
+    p = ODM_AT3 + z * p;
+    p = ODM_AT2 + z * p;
+    p = ODM_AT1 + z * p;
+    p = ODM_AT0 + z * p;
+    double r = u * p;
+    if (red) r = ODM_PI_6 + r;
+    if (inv) r = ODM_PI_2 - r;
+    return x < 0.0 ? -r : r;
+}
+static inline double odm_atan2(double y, double x)
+{
+    if (x != x || y != y) return x + y;
+    if (x > 0.0) return odm_atan(y / x);
+    if (x < 0.0) return y >= 0.0 ? odm_atan(y / x) + ODM_PI : odm_atan(y / x) - ODM_PI;
+    if (y > 0.0) return ODM_PI_2;
+    if (y < 0.0) return -ODM_PI_2;
+    return 0.0;
+}
+
 #endif

@@ -286,3 +286,50 @@ def gm_compute(ranges, a_cos, a_sin, pose=(0.0, 0.0, 1.0, 0.0), which="oracle", 
     else:
         nfree = gmapping_ref_lib().gmr_compute_map(*args)
     return n.reshape(sy, sx), v.reshape(sy, sx), acc.reshape(sy, sx, 2), int(nfree), nh.value
+
+
+# ---------------------------------------------------------------------------------------------- PL-ICP
+class PlParams(C.Structure):
+    """plo_params / pl_params (lesson3/src/plicp_odometry.cc:74-186 defaults)."""
+    _fields_ = [("max_angular_correction_deg", C.c_double), ("max_linear_correction", C.c_double),
+                ("epsilon_xy", C.c_double), ("epsilon_theta", C.c_double),
+                ("max_correspondence_dist", C.c_double), ("outliers_maxPerc", C.c_double),
+                ("outliers_adaptive_order", C.c_double), ("outliers_adaptive_mult", C.c_double),
+                ("max_iterations", C.c_int), ("use_point_to_line_distance", C.c_int),
+                ("outliers_remove_doubles", C.c_int), ("pad_", C.c_int)]
+
+
+_PL = None
+
+
+def plicp_lib():
+    global _PL
+    if _PL is None:
+        L = _lib(os.path.join(BUILD, "libplicp_oracle.so"))
+        L.plo_default_params.argtypes = [C.POINTER(PlParams)]
+        L.plo_icp.restype = _i
+        L.plo_icp.argtypes = [C.POINTER(PlParams), _i, C.c_double, C.c_double, _p, _p, _p, _i, _p,
+                              C.POINTER(_i), C.POINTER(_i), C.POINTER(C.c_double), _p]
+        _PL = L
+    return _PL
+
+
+def pl_default_params() -> PlParams:
+    p = PlParams()
+    plicp_lib().plo_default_params(C.byref(p))
+    return p
+
+
+def plicp(ref, sens, angle_min, angle_inc, first_guess=(0.0, 0.0, 0.0), params=None, reduce_threads=0):
+    """CPU restatement of CSM sm_icp (parity unpinned).  Returns dict(x, valid, iterations, nvalid, error)."""
+    L = plicp_lib()
+    p = params or pl_default_params()
+    ref = np.ascontiguousarray(ref, np.float64)
+    sens = np.ascontiguousarray(sens, np.float64)
+    g = np.ascontiguousarray(first_guess, np.float64)
+    x = np.zeros(3, np.float64)
+    it, nv, err = _i(), _i(), C.c_double()
+    hashes = np.zeros(64, np.int32)
+    ok = L.plo_icp(C.byref(p), ref.shape[0], float(angle_min), float(angle_inc), _fp(ref), _fp(sens), _fp(g),
+                   reduce_threads, _fp(x), C.byref(it), C.byref(nv), C.byref(err), _fp(hashes))
+    return dict(x=x, valid=bool(ok), iterations=it.value, nvalid=nv.value, error=err.value)

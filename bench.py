@@ -287,6 +287,98 @@ def run_gmapping(args, world, rank, dev):
     if world > 1:
         dist.destroy_process_group()
 
+PL_METRIC = "scan-pairs/sec (1081-beam) PL-ICP sm_icp (lesson3 parameters)"
+
+
+def plicp_pairs(num, seed, noise=0.01):
+    """Consecutive synthetic scans as LDP readings (LaserScanToLDP: -1 outside (0.1, 29.9) m)."""
+    from slam2d import synth
+    from slam2d.plicp import laser_scan_to_readings
+
+    rng = np.random.default_rng(seed)
+    phase = rng.uniform(0, 6.28)
+    gt = synth.trajectory(num + 1, phase)
+    R = synth.cast_ranges(gt, synth.world_segments()) + rng.normal(0, noise, (num + 1, synth.N_BEAMS))
+    R = laser_scan_to_readings(R, 0.1, 29.9)
+    ang = synth.beam_angles().astype(np.float64)
+    return R, float(ang[0]), float(ang[1] - ang[0])
+
+
+def plicp_cpu_baseline(seconds=10.0):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+
+    R, amin, inc = plicp_pairs(400, 4242)
+    done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < 400:
+        O.plicp(R[done], R[done + 1], amin, inc)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "scan-pairs/s", "cores": 1, "kind": "port",
+            "sample": f"{done} consecutive synthetic 1081-beam scan pairs, oracle/plicp_oracle.c -O3 single thread "
+                      "(exact polar-interval search; CSM's use_corr_tricks search is not available here)"}
+
+
+def run_plicp(args, world, rank, dev):
+    """lesson3 front-end: every step runs sm_icp for B independent scan pairs per GPU (B odometry
+    streams), inputs resident in HBM; replicas across GPUs (no exchange)."""
+    import torch
+    import torch.distributed as dist
+
+    from slam2d.plicp import PLICP
+
+    B, K, W = args.pairs, args.steps, args.warmup
+    R, amin, inc = plicp_pairs(B + K + W, 777 + rank)
+    d_R = torch.from_numpy(R).to(dev)
+    d_guess = torch.zeros((B, 3), dtype=torch.float64, device=dev)
+    d_out = torch.zeros((B, 48), dtype=torch.uint8, device=dev)
+    pl = PLICP(B, R.shape[1])
+    hs = torch.cuda.current_stream(dev).cuda_stream
+    nb = R.shape[1]
+    row = nb * 8
+
+    def step(t):  # pairs (t + b, t + b + 1), b < B: each pair a different stream position
+        pl.icp_batch_device(B, nb, amin, inc, d_R.data_ptr() + t * row, d_R.data_ptr() + (t + 1) * row,
+                            d_guess.data_ptr(), d_out.data_ptr(), hip_stream=hs)
+
+    for t in range(W):
+        step(t)
+    torch.cuda.synchronize()
+    pl.kernel_times(reset=True)
+    pl.set_timing(not args.no_timing)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(W, W + K):
+        step(t)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    pl.set_timing(False)
+    kms, kn = pl.kernel_times(reset=True)
+    t_max, total = aggregate_over_ranks(elapsed, float(B * K), dev)
+    if rank == 0:
+        cpu = None if (args.no_cpu_baseline or world > 1) else plicp_cpu_baseline()
+        out = {"metric": PL_METRIC, "value": round(total / t_max, 1), "unit": "scan-pairs/s", "n_gpus": world,
+               "steps": K, "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+               "config": {"workload": f"lesson3 plicp_odometry sm_icp, {B} independent 1081-beam scan pairs per GPU, "
+                                      "point-to-line, max 10 iterations", "config": "plicp", "pairs_per_gpu": B,
+                          "parallelism": f"replicas x{world}"},
+               "roofline": ({"bound": "latency", "kernel": "pl_icp_kernel", "avg_launch_ms": round(kms / kn, 5),
+                             "note": "compute/latency bound (no HBM roofline: 17 KB of input per pair)"}
+                            if kn else None),
+               "cpu_baseline": cpu}
+        if cpu:
+            out["speedup_vs_cpu_1core"] = round(out["value"] / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    pl.close()
+    if world > 1:
+        dist.destroy_process_group()
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -294,7 +386,8 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--streams", type=int, default=0, help="streams per GPU (0 = config default)")
-    ap.add_argument("--config", default="northstar", choices=sorted(CONFIGS) + ["gmapping"])
+    ap.add_argument("--config", default="northstar", choices=sorted(CONFIGS) + ["gmapping", "plicp"])
+    ap.add_argument("--pairs", type=int, default=2048, help="plicp: scan pairs per GPU per step")
     ap.add_argument("--particles", type=int, default=1024, help="gmapping: particles of the whole job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
@@ -319,6 +412,8 @@ def main():
 
     if args.config == "gmapping":
         return run_gmapping(args, world, rank, dev)
+    if args.config == "plicp":
+        return run_plicp(args, world, rank, dev)
     cfg = dict(CONFIGS[args.config])
     B = args.streams or cfg["streams"]
     K, W = args.steps, args.warmup

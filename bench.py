@@ -5,7 +5,7 @@ One step = one HectorSlamProcessor::update (match coarse->fine + log-odds raycas
 pyramid level) for each of B independent scan streams resident in HBM (inputs uploaded before the
 timed region).  Benchmark mode forces a map update on every scan (thresholds < 0).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--streams B] [--config northstar|c2|c3]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--streams B] [--config northstar|c2|c3|gmapping|plicp|karto|karto_loop]
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU; each rank runs its own B streams
 (replicas only -- the Hector path has no cross-stream exchange), barrier + synchronize around the
@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -379,6 +380,145 @@ def run_plicp(args, world, rank, dev):
     if world > 1:
         dist.destroy_process_group()
 
+KT_METRIC = {"karto": "matches/sec Karto ScanMatcher::MatchScan (coarse 16x16x21 + fine 3x3x11, 10 running scans)",
+             "karto_loop": "loop-closure matches/sec Karto ScanMatcher::MatchScan (coarse 101x101x21, 10-scan chain)"}
+
+
+def karto_setup(cfg, M, seed):
+    """Pool + batch description for one GPU.  karto: M sequential matches, each against the 10 scans
+    before it (running scans, Mapper.cpp:2040); karto_loop: M loop-closure candidates, each against a
+    10-scan chain from the first lap (TryCloseLoop's coarse call, Mapper.cpp:991)."""
+    import math
+
+    from slam2d import karto, synth
+
+    lz = karto.laser(synth.N_BEAMS, float(synth.ANGLE_MIN), float(synth.ANGLE_INC), 0.1, 12.0)
+    if cfg == "karto":
+        K = 10
+        R, T, Q = synth.karto_sequential(M, K, seed=seed)
+        ranges = np.concatenate([R, R[K:]])
+        poses = np.concatenate([T, Q[K:]])
+        query = np.arange(M + K, 2 * M + K, dtype=np.int32)
+        beg = (np.arange(M + 1) * K).astype(np.int32)
+        idx = (np.arange(M)[:, None] + np.arange(K)[None, :]).reshape(-1).astype(np.int32)
+        p = karto.default_params()
+        penalize, refine = True, True
+    else:
+        K = 10
+        QR, qp, qt, CR, CP = synth.karto_loop(M, K, seed=seed)
+        ranges = np.concatenate([QR, CR.reshape(-1, synth.N_BEAMS)])
+        poses = np.concatenate([qp, CP.reshape(-1, 3)])
+        query = np.arange(M, dtype=np.int32)
+        beg = (np.arange(M + 1) * K).astype(np.int32)
+        idx = (M + np.arange(M * K)).astype(np.int32)
+        p = karto.default_params(loop=True)
+        p.search_size = 10.0  # SURVEY.md C5: 101 x 101 x 21 coarse window at 0.05 m
+        penalize, refine = False, False
+    return lz, p, ranges, poses, query, beg, idx, K, penalize, refine
+
+
+def karto_cpu_baseline(cfg, seconds=10.0):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+
+    lz, p, ranges, poses, query, beg, idx, K, pen, ref = karto_setup(cfg, 32, 4242)
+    ol = O.KtLaser(lz.minimum_angle, lz.angular_resolution, lz.minimum_range, lz.range_threshold, lz.n_readings, 0)
+    op = O.KtParams(*[getattr(p, f) for f, _ in p._fields_])
+    done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < len(query):
+        b = idx[beg[done]:beg[done + 1]]
+        O.karto_match(ol, op, ranges[query[done]], poses[query[done]], ranges[b], poses[b], pen, ref)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "matches/s", "cores": 1, "kind": "port",
+            "sample": f"{done} synthetic {cfg} matches (1081 beams, {K} base scans), oracle/karto_oracle.c -O3 "
+                      "single thread (sequential restatement of open_karto's ScanMatcher; the library itself needs "
+                      "boost and is not built here)"}
+
+
+def run_karto(args, world, rank, dev):
+    """Karto correlative matcher (config 5): every step prepares the pool's scans (point readings) and
+    runs M independent MatchScan calls per GPU, inputs resident in HBM; replicas across GPUs."""
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+
+    from slam2d import karto
+
+    cfg = args.config
+    M = args.matches or (512 if cfg == "karto" else 32)
+    K, W = args.steps, args.warmup
+    lz, p, ranges, poses, query, beg, idx, NB, pen, ref = karto_setup(cfg, M, 777 + rank)
+    S = ranges.shape[0]
+    sm = karto.ScanMatcher(lz, p, max_matches=M, max_scans=S, max_base=NB)
+    d_r = torch.from_numpy(ranges).to(dev)
+    d_p = torch.from_numpy(poses).to(dev)
+    d_q, d_b, d_i = (torch.from_numpy(a).to(dev) for a in (query, beg, idx))
+    d_res = torch.zeros(M * C.sizeof(karto.KtResult), dtype=torch.uint8, device=dev)
+    hs = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        sm.set_scans_device(0, S, d_r.data_ptr(), d_p.data_ptr(), hip_stream=hs)
+        sm.match_batch_device(M, d_q.data_ptr(), d_b.data_ptr(), d_i.data_ptr(), d_res.data_ptr(), pen, ref,
+                              hip_stream=hs)
+
+    for _ in range(W):
+        step()
+    torch.cuda.synchronize()
+    sm.kernel_times(reset=True)
+    sm.set_timing(not args.no_timing)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    sm.set_timing(False)
+    kt = sm.kernel_times(reset=True)
+    res = karto.results_from_bytes(d_res.cpu().numpy())
+    t_max, total = aggregate_over_ranks(elapsed, float(M * K), dev)
+    if rank == 0:
+        cpu = None if (args.no_cpu_baseline or world > 1) else karto_cpu_baseline(cfg)
+        info = sm.info
+        coarse_ms, coarse_n = kt.get("kt_coarse_kernel", (0.0, 0))
+        nA = 21
+        npos = ((info["side"] - 1) // 2 + 1) ** 2
+        roof = None
+        if coarse_n and not args.no_timing:
+            # algorithmic bytes of one coarse launch: every (pose, point) lookup reads one grid byte,
+            # plus the 16-byte local point and 1-byte flag each (angle, tile) workgroup reads per point
+            tiles = -(-int(math.sqrt(npos)) // 16) ** 2
+            pts = float(np.isfinite(ranges[query]).sum(axis=1).mean())
+            per_launch = M * (npos * nA * pts + nA * tiles * pts * 17.0)
+            avg_s = coarse_ms / coarse_n * 1e-3
+            ach = per_launch / avg_s / 1e9
+            roof = {"bound": "hbm", "kernel": "kt_coarse_kernel", "achieved": round(ach, 1), "peak": 8000.0,
+                    "unit": "GB/s", "frac": round(ach / 8000.0, 4), "traffic": None,
+                    "avg_launch_ms": round(coarse_ms / coarse_n, 5),
+                    "note": "achieved = lookup bytes (1 B per pose x point) / launch time; the correlation grids "
+                            "are L2 / Infinity-Cache resident, so this is a gather rate, not DRAM traffic"}
+        out = {"metric": KT_METRIC[cfg], "value": round(total / t_max, 1), "unit": "matches/s", "n_gpus": world,
+               "steps": K, "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+               "config": {"workload": f"lesson6 karto_slam {cfg}: {M} independent MatchScan calls per GPU, "
+                                      f"{NB} base scans each, 1081 beams, grid {info['grid_size']}^2",
+                          "config": cfg, "matches_per_gpu": M, "parallelism": f"replicas x{world}",
+                          "kernel_ms": {k: round(v[0], 3) for k, v in kt.items()}},
+               "roofline": roof, "cpu_baseline": cpu,
+               "ok_results": int((res["status"] == 0).sum())}
+        if cpu:
+            out["speedup_vs_cpu_1core"] = round(out["value"] / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    sm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -386,8 +526,9 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--streams", type=int, default=0, help="streams per GPU (0 = config default)")
-    ap.add_argument("--config", default="northstar", choices=sorted(CONFIGS) + ["gmapping", "plicp"])
+    ap.add_argument("--config", default="northstar", choices=sorted(CONFIGS) + ["gmapping", "plicp", "karto", "karto_loop"])
     ap.add_argument("--pairs", type=int, default=2048, help="plicp: scan pairs per GPU per step")
+    ap.add_argument("--matches", type=int, default=0, help="karto: MatchScan calls per GPU per step (0 = default)")
     ap.add_argument("--particles", type=int, default=1024, help="gmapping: particles of the whole job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
@@ -414,6 +555,8 @@ def main():
         return run_gmapping(args, world, rank, dev)
     if args.config == "plicp":
         return run_plicp(args, world, rank, dev)
+    if args.config in ("karto", "karto_loop"):
+        return run_karto(args, world, rank, dev)
     cfg = dict(CONFIGS[args.config])
     B = args.streams or cfg["streams"]
     K, W = args.steps, args.warmup

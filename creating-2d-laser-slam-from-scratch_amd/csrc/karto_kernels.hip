@@ -1,0 +1,868 @@
+// karto_kernels.hip -- MI355X kernels of the Karto correlative scan matcher (lesson6, config 5).
+//
+// One MatchScan (lesson6/lib/open_karto/src/Mapper.cpp:184-300) per "match slot"; a launch serves a
+// whole batch of independent matches (a loop-closure candidate batch, or many robots' sequential
+// matches).  Kernels, in stream order:
+//   kt_prepare_kernel  one workgroup per pooled scan: LocalizedRangeScan::Update point readings
+//                      (Karto.h:5362-5404, order-preserving compaction), the points in the scan's own
+//                      frame (Transform::InverseTransformPose, Karto.h:2894-2901) and the
+//                      viewpoint-independent half of FindValidPoints (Mapper.cpp:755-811): the
+//                      "first point" reset events, found by one lane walking the points in LDS.
+//   kt_begin_kernel    per match: centre the correlation grid on the query's pose (MatchScan 1-4).
+//   kt_build_kernel    per (match, base scan): the viewpoint test of FindValidPoints, then AddScan +
+//                      SmearPoint (Mapper.cpp:716-748, Mapper.h:971-1005) as a byte-wise max of the
+//                      smear kernel into the grid (32-bit compare-and-swap words).  Order-free because
+//                      the kernel's only 100 is its centre (checked at kt_create).
+//   kt_coarse_kernel   per (match, angle, 16x16 position tile): GridIndexLookup::ComputeOffsets for one
+//                      angle into LDS (Karto.h:6455-6501), then GetResponse (Mapper.cpp:819-856) for the
+//                      tile's 256 positions -- each lane owns 4 positions two cells apart and reads
+//                      them with ONE unaligned 8-byte gather per point (bytes 0, 2, 4, 6), summed as
+//                      packed 16-bit lanes; the 4 waves split the points.  Penalty (Mapper.cpp:
+//                      398-416), responses in the reference's pose order, per-position max over angles
+//                      (the search-space probability grid) and the best response by 64-bit atomic max.
+//   kt_select_kernel   per match: poses tying the best (DoubleEqual) compacted in pose order and
+//                      averaged by one lane in that order (Mapper.cpp:456-487), the positional
+//                      covariance (Mapper.cpp:535-626), response expansion (Mapper.cpp:244-271).
+//   kt_fine_kernel     per match: the fine CorrelateScan (3x3 positions x fine angles) and
+//                      ComputeAngularCovariance (Mapper.cpp:638-690) in one workgroup.
+//   kt_build_kernel    again with clear = 1: zero exactly the words the smear touched, so the slot's
+//                      grid is clean for the next match without a 6 MB memset.
+// All arithmetic is double, with -ffp-contract=off and the deterministic sin / cos / atan2 of
+// detmath.h; the CPU restatement oracle/karto_oracle.c evaluates the same sequence (bit-exact parity).
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/slam2d/karto.h"
+#include "detmath.h"
+
+namespace s2d {
+
+constexpr int KT_THREADS = 256;
+constexpr int KT_MAX_READINGS = 4096;
+constexpr int KT_TILE = 16;
+constexpr int KT_FINE_MAX_ANG = 64;
+constexpr int KT_INVALID = INT_MIN;  // INVALID_SCAN: any position index + this is negative -> skipped
+constexpr double KT_PI = 3.14159265358979323846;
+constexpr double KT_2PI = 6.28318530717958647692;
+constexpr double KT_TOL = 1e-06;
+constexpr double KT_MAX_VARIANCE = 500.0;
+constexpr double KT_GAIN = 0.2;  // DISTANCE_PENALTY_GAIN == ANGLE_PENALTY_GAIN (Mapper.cpp:37-38)
+constexpr int KT_OCC = 100;
+
+// Host-computed geometry of one ScanMatcher (ScanMatcher::Create + CorrelateScan's search spaces).
+struct KtGeom {
+    double scale, res;                 // 1 / resolution, GetResolution() = 1 / scale
+    int grid_size, border, width, height, ws, data_size;
+    int side, probs_ws, half, ksize;
+    int n;                             // readings per scan
+    int nxy, tiles;                    // coarse positions per axis, 16-position tiles per axis
+    int npass;                         // 1, or 4 with response expansion
+    int nang[4];
+    double aoff[4];                    // coarse angle offset per pass
+    double coff, cres;                 // coarse search offset / resolution
+    double foff;                       // fine search offset (resolution = res)
+    int fn, fnang;                     // fine positions per axis, fine angles
+    double faoff, fares;               // fine angle offset / resolution
+    double min_angle, ang_res, min_range, range_thr;
+    double dvp, avp, mdp, map_;        // penalties
+    double cares;                      // coarse angle resolution
+    int use_expansion;
+    int max_poses;
+    size_t grid_stride;                // bytes per match slot grid
+};
+
+struct KtPool {
+    const double *ranges;  // [S][n]
+    const double *poses;   // [S][3]
+    int *npts;             // [S]
+    double2 *pts;          // [S][n] world point readings
+    double2 *loc;          // [S][n] points in the scan's frame
+    unsigned char *bad;    // [S][n] raw reading k (k < npts) is NaN / inf (ComputeOffsets, Karto.h:6476-6481)
+    int2 *evt;             // [S][n] (closing reset event, its first point) of point k, or (-1, -1)
+};
+
+struct KtState {
+    double center[3];
+    double gox, goy;
+    double mean[3];
+    double cov[9];
+    double best;
+    unsigned long long best_bits;
+    int query, npts, pass, status;
+};
+
+// ---- Math.h (K/include/open_karto/Math.h:87-233) ----------------------------------------------
+__device__ __forceinline__ double kt_round(double v) { return v >= 0.0 ? floor(v + 0.5) : ceil(v - 0.5); }
+__device__ __forceinline__ bool kt_deq(double a, double b)
+{
+    const double d = a - b;
+    return d < 0.0 ? d >= -KT_TOL : d <= KT_TOL;
+}
+__device__ __forceinline__ double kt_max(double a, double b) { return a > b ? a : b; }
+__device__ __forceinline__ double kt_sq(double v) { return v * v; }
+__device__ inline double kt_norm_angle(double a)
+{
+    if (!isfinite(a)) return a;  // the reference would spin; a non-finite heading is passed through
+    while (a < -KT_PI) {
+        if (a < -KT_2PI) a += (double)(uint32_t)(a / -KT_2PI) * KT_2PI;
+        else a += KT_2PI;
+    }
+    while (a > KT_PI) {
+        if (a > KT_2PI) a -= (double)(uint32_t)(a / KT_2PI) * KT_2PI;
+        else a -= KT_2PI;
+    }
+    return a;
+}
+__device__ inline double kt_norm_angle_diff(double minuend, double subtrahend)
+{
+    while (minuend - subtrahend < -KT_PI) minuend += KT_2PI;
+    while (minuend - subtrahend > KT_PI) minuend -= KT_2PI;
+    return minuend;
+}
+__device__ __forceinline__ int kt_w2g(double w, double o, double scale) { return (int)kt_round((w - o) * scale); }
+
+__device__ __forceinline__ unsigned long long kt_bits(double v) { return (unsigned long long)__double_as_longlong(v); }
+__device__ __forceinline__ double kt_dbl(unsigned long long b) { return __longlong_as_double((long long)b); }
+
+// block-wide exclusive scan of v (256 threads); total returned through *total
+__device__ __forceinline__ int kt_block_exscan(int v, int *sw, int *total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += t;
+    }
+    if (lane == 63) sw[w] = inc;
+    __syncthreads();
+    int woff = 0;
+    for (int i = 0; i < w; ++i) woff += sw[i];
+    *total = sw[0] + sw[1] + sw[2] + sw[3];
+    __syncthreads();
+    return woff + inc - v;
+}
+
+__device__ __forceinline__ int kt_block_max_int(int v, int *sw)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+    if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const int r = max(max(sw[0], sw[1]), max(sw[2], sw[3]));
+    __syncthreads();
+    return r;
+}
+
+// rotation part of Transform(sensorPose).InverseTransformPose: Matrix3::FromAxisAngle(0, 0, 1, 0 - h)
+// (Karto.h:2392-2420, :2909-2935) and Matrix3 * Pose2 (Karto.h:2574-2583)
+__device__ __forceinline__ void kt_inv_rot(double h, double r[6])
+{
+    const double rad = 0.0 - h;
+    const double c = sdm_cos(rad), s = sdm_sin(rad);
+    const double omc = 1.0 - c;
+    const double zomc = (0.0 * 0.0) * omc;
+    r[0] = 0.0 * omc + c;
+    r[1] = zomc - 1.0 * s;
+    r[2] = zomc + 0.0 * s;
+    r[3] = zomc + 1.0 * s;
+    r[4] = 0.0 * omc + c;
+    r[5] = zomc - 0.0 * s;
+}
+
+// =================================================================================================
+// kt_prepare_kernel: pooled scans -> point readings, local points, reset events
+// =================================================================================================
+__global__ void __launch_bounds__(KT_THREADS)
+kt_prepare_kernel(KtGeom g, KtPool P, int first)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char kt_smem[];
+    double2 *spts = reinterpret_cast<double2 *>(kt_smem);       // [n]
+    int *sev = reinterpret_cast<int *>(spts + g.n);              // [n] reset events
+    __shared__ int sw[4];
+    __shared__ int s_nev;
+
+    const int s = first + blockIdx.x;
+    const int tid = threadIdx.x;
+    const int n = g.n;
+    const double *raw = P.ranges + (size_t)s * n;
+    const double px = P.poses[3 * s], py = P.poses[3 * s + 1], ph = P.poses[3 * s + 2];
+
+    // order-preserving compaction of the readings InRange(r, minimumRange, rangeThreshold)
+    const int chunk = (n + KT_THREADS - 1) / KT_THREADS;
+    const int i0 = min(tid * chunk, n), i1 = min(i0 + chunk, n);
+    int cnt = 0;
+    for (int i = i0; i < i1; ++i) {
+        const double r = raw[i];
+        cnt += (r >= g.min_range && r <= g.range_thr) ? 1 : 0;
+    }
+    int npts;
+    int k = kt_block_exscan(cnt, sw, &npts);
+    double R[6];
+    kt_inv_rot(ph, R);
+    const double dth = kt_norm_angle(0.0 - ph);
+    double2 *pts = P.pts + (size_t)s * n;
+    double2 *loc = P.loc + (size_t)s * n;
+    for (int i = i0; i < i1; ++i) {
+        const double r = raw[i];
+        if (!(r >= g.min_range && r <= g.range_thr)) continue;
+        const double angle = ph + g.min_angle + (double)(uint32_t)i * g.ang_res;
+        const double x = px + (r * sdm_cos(angle));
+        const double y = py + (r * sdm_sin(angle));
+        pts[k] = make_double2(x, y);
+        spts[k] = make_double2(x, y);
+        const double dx = x - px, dy = y - py;
+        const double lx = R[0] * dx + R[1] * dy + R[2] * dth;
+        const double ly = R[3] * dx + R[4] * dy + R[5] * dth;
+        loc[k] = make_double2(lx, ly);
+        ++k;
+    }
+    unsigned char *bad = P.bad + (size_t)s * n;
+    for (int j = tid; j < npts; j += KT_THREADS) {
+        const double r = raw[j];  // the reference indexes the raw readings with the point index
+        bad[j] = (isnan(r) || isinf(r)) ? 1 : 0;
+    }
+    if (tid == 0) P.npts[s] = npts;
+    __syncthreads();
+    // FindValidPoints' reset events (the viewpoint-independent walk), one lane
+    if (tid == 0) {
+        const double min_sq = 0.1 * 0.1;
+        int nev = 0;
+        if (npts > 0) {
+            double fx = spts[0].x, fy = spts[0].y;
+            for (int j = 0; j < npts; ++j) {
+                const double2 c = spts[j];
+                const double dx = fx - c.x, dy = fy - c.y;
+                if (dx * dx + dy * dy > min_sq) {
+                    sev[nev++] = j;
+                    fx = c.x;
+                    fy = c.y;
+                }
+            }
+        }
+        s_nev = nev;
+    }
+    __syncthreads();
+    const int nev = s_nev;
+    int2 *evt = P.evt + (size_t)s * n;
+    for (int j = tid; j < npts; j += KT_THREADS) {
+        int lo = 0, hi = nev;  // first event > j
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sev[mid] > j) hi = mid;
+            else lo = mid + 1;
+        }
+        evt[j] = lo < nev ? make_int2(sev[lo], lo > 0 ? sev[lo - 1] : 0) : make_int2(-1, -1);
+    }
+}
+
+// =================================================================================================
+// kt_begin_kernel: centre the correlation grid on the scan pose (MatchScan steps 1-4)
+// =================================================================================================
+__global__ void __launch_bounds__(KT_THREADS)
+kt_begin_kernel(KtGeom g, KtPool P, const int *__restrict__ query, KtState *st, unsigned long long *posmax)
+{
+    const int m = blockIdx.x;
+    const int q = query[m];
+    if (threadIdx.x == 0) {
+        KtState &S = st[m];
+        S.center[0] = P.poses[3 * q];
+        S.center[1] = P.poses[3 * q + 1];
+        S.center[2] = P.poses[3 * q + 2];
+        S.gox = S.center[0] - (0.5 * (g.grid_size - 1) * g.res);
+        S.goy = S.center[1] - (0.5 * (g.grid_size - 1) * g.res);
+        S.best_bits = 0ull;
+        S.best = 0.0;
+        S.query = q;
+        S.npts = P.npts[q];
+        S.pass = 0;
+        S.status = KT_OK;
+    }
+    unsigned long long *pm = posmax + (size_t)m * g.nxy * g.nxy;
+    for (int i = threadIdx.x; i < g.nxy * g.nxy; i += KT_THREADS) pm[i] = 0ull;
+}
+
+// =================================================================================================
+// kt_build_kernel: AddScans (clear = 0) / zero the same footprints (clear = 1)
+// =================================================================================================
+__device__ __forceinline__ unsigned kt_bytemax4(unsigned a, unsigned b)
+{
+    unsigned r = 0;
+#pragma unroll
+    for (int t = 0; t < 32; t += 8) r |= max((a >> t) & 0xFFu, (b >> t) & 0xFFu) << t;
+    return r;
+}
+
+__global__ void __launch_bounds__(KT_THREADS)
+kt_build_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int *__restrict__ bbeg,
+                const int *__restrict__ bidx, const unsigned char *__restrict__ kernel, unsigned char *grids, int clear)
+{
+    __shared__ unsigned char sk[41 * 41];
+    const int m = blockIdx.y;
+    const int j = blockIdx.x;
+    const int b0 = bbeg[m], b1 = bbeg[m + 1];
+    if (b0 + j >= b1) return;
+    const int s = bidx[b0 + j];
+    for (int i = threadIdx.x; i < g.ksize * g.ksize; i += KT_THREADS) sk[i] = kernel[i];
+    __syncthreads();
+    const KtState &S = st[m];
+    const double vx = S.center[0], vy = S.center[1];
+    const double gox = S.gox, goy = S.goy;
+    const int npts = P.npts[s];
+    const double2 *pts = P.pts + (size_t)s * g.n;
+    const int2 *evt = P.evt + (size_t)s * g.n;
+    unsigned char *grid = grids + (size_t)m * g.grid_stride;
+    unsigned *gw = reinterpret_cast<unsigned *>(grid);
+    const int h = g.half, ks = g.ksize;
+    for (int k = threadIdx.x; k < npts; k += KT_THREADS) {
+        const int2 e = evt[k];
+        if (e.x < 0) continue;
+        const double2 f = pts[e.y], c = pts[e.x];
+        const double a = vy - f.y;
+        const double b = f.x - vx;
+        const double cc = f.y * vx - f.x * vy;
+        const double ss = c.x * a + c.y * b + cc;
+        if (ss < 0.0) continue;  // wrong side of the viewpoint (Mapper.cpp:795-799)
+        const double2 p = pts[k];
+        const int gx = kt_w2g(p.x, gox, g.scale), gy = kt_w2g(p.y, goy, g.scale);
+        if (!(gx >= 0 && gx < g.grid_size) || !(gy >= 0 && gy < g.grid_size)) continue;
+        const int cx = gx + g.border, cy = gy + g.border;
+        if (!clear && grid[cx + cy * g.ws] == KT_OCC) continue;  // value already set (Mapper.cpp:735-739)
+        for (int jj = -h; jj <= h; ++jj) {
+            const int row = (cx - h) + (cy + jj) * g.ws;  // first footprint byte of this row
+            const unsigned char *krow = sk + ks * (jj + h);
+            const int w0 = row >> 2, w1 = (row + ks - 1) >> 2;
+            for (int w = w0; w <= w1; ++w) {
+                if (clear) {
+                    gw[w] = 0u;
+                    continue;
+                }
+                unsigned want = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int col = w * 4 + t - row;
+                    if (col >= 0 && col < ks) want |= (unsigned)krow[col] << (8 * t);
+                }
+                if (want == 0u) continue;
+                unsigned old = gw[w];
+                while (true) {
+                    const unsigned nv = kt_bytemax4(old, want);
+                    if (nv == old) break;
+                    const unsigned prev = atomicCAS(gw + w, old, nv);
+                    if (prev == old) break;
+                    old = prev;
+                }
+            }
+        }
+    }
+}
+
+// =================================================================================================
+// kt_coarse_kernel: GetResponse over a 16x16 tile of positions for one angle
+// =================================================================================================
+__global__ void __launch_bounds__(KT_THREADS)
+kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict__ grids, double *resp,
+                 unsigned long long *posmax, int count, int pass, int penalize)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char kt_smem[];
+    int *soff = reinterpret_cast<int *>(kt_smem);  // [npts]
+    __shared__ unsigned scnt[4][KT_THREADS];
+    __shared__ double sbest[4];
+
+    const int nA = g.nang[pass];
+    const int T2 = g.tiles * g.tiles;
+    const int W = nA * T2;
+    // XCD-aware: all work of one match runs on one XCD (blocks are dealt round-robin to the 8 XCDs)
+    const int b = blockIdx.x;
+    const int xcd = b & 7, q8 = b >> 3;
+    const int grp = q8 / W, w = q8 - grp * W;
+    const int m = grp * 8 + xcd;
+    if (m >= count) return;
+    KtState &S = st[m];
+    if (S.pass != pass) return;
+    const int a = w / T2, t = w - a * T2;
+    const int ty = t / g.tiles, tx = t - ty * g.tiles;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+    const double cxs = S.center[0], cys = S.center[1], chs = S.center[2];
+    const double gox = S.gox, goy = S.goy;
+    const double aoff = g.aoff[pass];
+    const double start = chs - aoff;
+    const double angle = start + (double)(uint32_t)a * g.cares;
+    const double cs = sdm_cos(angle), sn = sdm_sin(angle);
+    const int q = S.query, npts = S.npts;
+    const double2 *loc = P.loc + (size_t)q * g.n;
+    const unsigned char *bad = P.bad + (size_t)q * g.n;
+    for (int k = tid; k < npts; k += KT_THREADS) {
+        int o = KT_INVALID;
+        if (!bad[k]) {
+            const double2 l = loc[k];
+            const double ox = cs * l.x - sn * l.y;
+            const double oy = sn * l.x + cs * l.y;
+            const int gx = kt_w2g(ox + gox, gox, g.scale), gy = kt_w2g(oy + goy, goy, g.scale);
+            o = gx + gy * g.ws;
+        }
+        soff[k] = o;
+    }
+    // this lane's 4 positions: row iy, columns ix0 .. ix0 + 3
+    const int iy = ty * KT_TILE + (lane >> 2);
+    const int ix0 = tx * KT_TILE + (lane & 3) * 4;
+    const double startX = -g.coff;
+    int gpos[4];
+    bool fast = true;
+    {
+        const double y = startX + (double)(uint32_t)iy * g.cres;
+        const int gy = kt_w2g(cys + y, goy, g.scale) + g.border;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ix = ix0 + j;
+            gpos[j] = 0;
+            if (ix < g.nxy && iy < g.nxy) {
+                const double x = startX + (double)(uint32_t)ix * g.cres;
+                const int gx = kt_w2g(cxs + x, gox, g.scale) + g.border;
+                if (gx < 0 || gx >= g.width || gy < 0 || gy >= g.height) {
+                    S.status = KT_ERANGE;  // GridIndex would throw (Karto.h:4488-4499)
+                    continue;
+                }
+                gpos[j] = gx + gy * g.ws;
+                if (gpos[j] != gpos[0] + 2 * j) fast = false;
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned ds = (unsigned)g.data_size;
+    const unsigned lim = ds - 6u;
+    const unsigned char *grid = grids + (size_t)m * g.grid_stride;
+    unsigned c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    unsigned acc01 = 0, acc23 = 0;
+    int since = 0;
+    if (fast) {
+        const int base = gpos[0];
+        for (int k = wave; k < npts; k += 4) {
+            const int bi = base + soff[k];
+            if ((unsigned)bi < lim) {
+                uint2 v;
+                __builtin_memcpy(&v, grid + bi, 8);
+                acc01 += v.x & 0x00FF00FFu;
+                acc23 += v.y & 0x00FF00FFu;
+            } else {
+                if ((unsigned)bi < ds) c0 += grid[bi];
+                if ((unsigned)(bi + 2) < ds) c1 += grid[bi + 2];
+                if ((unsigned)(bi + 4) < ds) c2 += grid[bi + 4];
+                if ((unsigned)(bi + 6) < ds) c3 += grid[bi + 6];
+            }
+            if (++since == 512) {  // 512 * 100 < 65536: flush the packed 16-bit sums
+                c0 += acc01 & 0xFFFFu; c1 += acc01 >> 16; c2 += acc23 & 0xFFFFu; c3 += acc23 >> 16;
+                acc01 = acc23 = 0;
+                since = 0;
+            }
+        }
+        c0 += acc01 & 0xFFFFu; c1 += acc01 >> 16; c2 += acc23 & 0xFFFFu; c3 += acc23 >> 16;
+    } else {
+        for (int k = wave; k < npts; k += 4) {
+            const int o = soff[k];
+            const int i0 = gpos[0] + o, i1 = gpos[1] + o, i2 = gpos[2] + o, i3 = gpos[3] + o;
+            if ((unsigned)i0 < ds) c0 += grid[i0];
+            if ((unsigned)i1 < ds) c1 += grid[i1];
+            if ((unsigned)i2 < ds) c2 += grid[i2];
+            if ((unsigned)i3 < ds) c3 += grid[i3];
+        }
+    }
+    scnt[wave][lane * 4 + 0] = c0;
+    scnt[wave][lane * 4 + 1] = c1;
+    scnt[wave][lane * 4 + 2] = c2;
+    scnt[wave][lane * 4 + 3] = c3;
+    __syncthreads();
+    // one thread per position of the tile
+    const unsigned total = scnt[0][tid] + scnt[1][tid] + scnt[2][tid] + scnt[3][tid];
+    const int pl = tid >> 2, pj = tid & 3;
+    const int piy = ty * KT_TILE + (pl >> 2);
+    const int pix = tx * KT_TILE + (pl & 3) * 4 + pj;
+    double best = 0.0;
+    if (piy < g.nxy && pix < g.nxy) {
+        double response = 0.0;
+        if (npts > 0) response = (double)total / (double)(uint32_t)(npts * KT_OCC);
+        if (penalize && !kt_deq(response, 0.0)) {
+            const double x = startX + (double)(uint32_t)pix * g.cres;
+            const double y = startX + (double)(uint32_t)piy * g.cres;
+            const double sqd = kt_sq(x) + kt_sq(y);
+            double dp = 1.0 - (KT_GAIN * sqd / g.dvp);
+            dp = kt_max(dp, g.mdp);
+            const double sqa = kt_sq(angle - chs);
+            double ap = 1.0 - (KT_GAIN * sqa / g.avp);
+            ap = kt_max(ap, g.map_);
+            response *= (dp * ap);
+        }
+        const size_t pos = (size_t)piy * g.nxy + pix;
+        resp[(size_t)m * g.max_poses + pos * nA + a] = response;
+        atomicMax(posmax + (size_t)m * g.nxy * g.nxy + pos, kt_bits(response));
+        best = response;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) best = kt_max(best, __shfl_xor(best, off, 64));
+    if (lane == 0) sbest[wave] = best;
+    __syncthreads();
+    if (tid == 0) {
+        const double bb = kt_max(kt_max(sbest[0], sbest[1]), kt_max(sbest[2], sbest[3]));
+        atomicMax(&S.best_bits, kt_bits(bb));
+    }
+}
+
+// =================================================================================================
+// kt_select_kernel: best, tie average, positional covariance, response expansion
+// =================================================================================================
+__global__ void __launch_bounds__(KT_THREADS)
+kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigned long long *posmax, int *tie_idx,
+                 double4 *tie_val, int pass, int refine, kt_result *out)
+{
+    __shared__ int sw[4];
+    __shared__ int s_n;
+    __shared__ double s_mean[3];
+    __shared__ int s_err;
+    const int m = blockIdx.x;
+    KtState &S = st[m];
+    if (S.pass != pass) return;
+    const int tid = threadIdx.x;
+    const int nA = g.nang[pass];
+    const int nxy = g.nxy;
+    const int np = nxy * nxy * nA;
+    const double best = kt_dbl(S.best_bits);
+    const double *r = resp + (size_t)m * g.max_poses;
+    int *ti = tie_idx + (size_t)m * g.max_poses;
+    double4 *tv = tie_val + (size_t)m * g.max_poses;
+    const double cx = S.center[0], cy = S.center[1], ch = S.center[2];
+    const double startX = -g.coff;
+    const double astart = ch - g.aoff[pass];
+    if (tid == 0) {
+        s_n = 0;
+        s_err = 0;
+    }
+    __syncthreads();
+    // poses with DoubleEqual(response, best), in pose order
+    for (int base = 0; base < np; base += KT_THREADS) {
+        const int i = base + tid;
+        const int f = (i < np && kt_deq(r[i], best)) ? 1 : 0;
+        int tot;
+        const int pre = kt_block_exscan(f, sw, &tot);
+        const int n0 = s_n;
+        if (f) ti[n0 + pre] = i;
+        __syncthreads();
+        if (tid == 0) s_n = n0 + tot;
+        __syncthreads();
+    }
+    const int nt = s_n;
+    for (int t = tid; t < nt; t += KT_THREADS) {
+        const int i = ti[t];
+        const int a = i % nA, pos = i / nA;
+        const int ix = pos % nxy, iy = pos / nxy;
+        const double x = cx + (startX + (double)(uint32_t)ix * g.cres);
+        const double y = cy + (startX + (double)(uint32_t)iy * g.cres);
+        const double h = kt_norm_angle(astart + (double)(uint32_t)a * g.cares);
+        tv[t] = make_double4(x, y, sdm_cos(h), sdm_sin(h));
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double ax = 0.0, ay = 0.0, tx = 0.0, ty = 0.0;
+        for (int t = 0; t < nt; ++t) {
+            const double4 v = tv[t];
+            ax += v.x;
+            ay += v.y;
+            tx += v.z;
+            ty += v.w;
+        }
+        if (nt > 0) {
+            ax /= nt;
+            ay /= nt;
+            tx /= nt;
+            ty /= nt;
+            s_mean[0] = ax;
+            s_mean[1] = ay;
+            s_mean[2] = sdm_atan2(ty, tx);
+        } else {
+            s_mean[0] = s_mean[1] = s_mean[2] = 0.0;
+            s_err = 1;
+        }
+    }
+    __syncthreads();
+    // ComputePositionalCovariance over the search-space probability grid
+    double cov[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    const double pgox = cx - g.coff, pgoy = cy - g.coff;
+    if (best < KT_TOL) {
+        cov[0] = KT_MAX_VARIANCE;
+        cov[4] = KT_MAX_VARIANCE;
+        cov[8] = 4 * kt_sq(g.cares);
+    } else {
+        const unsigned long long *pm = posmax + (size_t)m * nxy * nxy;
+        const double lo = best - 0.1;
+        __syncthreads();
+        if (tid == 0) s_n = 0;
+        __syncthreads();
+        const int npos = nxy * nxy;
+        for (int base = 0; base < npos; base += KT_THREADS) {
+            const int i = base + tid;
+            int f = 0;
+            double val = 0.0;
+            if (i < npos) {
+                const int ix = i % nxy, iy = i / nxy;
+                const double x = cx + (startX + (double)(uint32_t)ix * g.cres);
+                const double y = cy + (startX + (double)(uint32_t)iy * g.cres);
+                const int pgx = kt_w2g(x, pgox, g.scale), pgy = kt_w2g(y, pgoy, g.scale);
+                if (pgx < 0 || pgx >= g.side || pgy < 0 || pgy >= g.side) {
+                    s_err = 2;  // "Index out of range in probability search" (Mapper.cpp:446)
+                } else {
+                    // the probability cell holds the max over every pose that lands in it: this
+                    // position and any neighbour whose coordinates round to the same cell
+                    unsigned long long v = pm[i];
+                    for (int dy = -1; dy <= 1; ++dy)
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            const int jx = ix + dx, jy = iy + dy;
+                            if ((dx == 0 && dy == 0) || jx < 0 || jy < 0 || jx >= nxy || jy >= nxy) continue;
+                            const double xx = cx + (startX + (double)(uint32_t)jx * g.cres);
+                            const double yy = cy + (startX + (double)(uint32_t)jy * g.cres);
+                            if (kt_w2g(xx, pgox, g.scale) == pgx && kt_w2g(yy, pgoy, g.scale) == pgy)
+                                v = max(v, pm[jy * nxy + jx]);
+                        }
+                    val = kt_dbl(v);
+                    f = val >= lo ? 1 : 0;
+                }
+            }
+            int tot;
+            const int pre = kt_block_exscan(f, sw, &tot);
+            const int n0 = s_n;
+            if (f) {
+                const int ix = i % nxy, iy = i / nxy;
+                tv[n0 + pre] = make_double4(startX + (double)(uint32_t)ix * g.cres,
+                                            startX + (double)(uint32_t)iy * g.cres, val, 0.0);
+            }
+            __syncthreads();
+            if (tid == 0) s_n = n0 + tot;
+            __syncthreads();
+        }
+        if (tid == 0) {
+            const int nc = s_n;
+            double axx = 0, axy = 0, ayy = 0, norm = 0;
+            const double dx = s_mean[0] - cx, dy = s_mean[1] - cy;
+            for (int t = 0; t < nc; ++t) {
+                const double4 v = tv[t];
+                const double x = v.x, y = v.y, response = v.z;
+                norm += response;
+                axx += (kt_sq(x - dx) * response);
+                axy += ((x - dx) * (y - dy) * response);
+                ayy += (kt_sq(y - dy) * response);
+            }
+            if (norm > KT_TOL) {
+                double vxx = axx / norm, vxy = axy / norm, vyy = ayy / norm;
+                const double vtt = 4 * kt_sq(g.cares);
+                const double minxx = 0.1 * kt_sq(g.cres), minyy = 0.1 * kt_sq(g.cres);
+                vxx = kt_max(vxx, minxx);
+                vyy = kt_max(vyy, minyy);
+                const double mult = 1.0 / best;
+                cov[0] = vxx * mult;
+                cov[1] = vxy * mult;
+                cov[3] = vxy * mult;
+                cov[4] = vyy * mult;
+                cov[8] = vtt;
+            }
+            if (kt_deq(cov[0], 0.0)) cov[0] = KT_MAX_VARIANCE;
+            if (kt_deq(cov[4], 0.0)) cov[4] = KT_MAX_VARIANCE;
+        }
+    }
+    if (tid == 0) {
+        const double clamped = best > 1.0 ? 1.0 : best;
+        for (int i = 0; i < 3; ++i) S.mean[i] = s_mean[i];
+        for (int i = 0; i < 9; ++i) S.cov[i] = cov[i];
+        S.best = clamped;
+        if (s_err) S.status = KT_ERANGE;
+        if (g.use_expansion && pass + 1 < g.npass && kt_deq(clamped, 0.0)) {
+            S.pass = pass + 1;  // MatchScan: widen the angular window by 20 degrees and retry
+            S.best_bits = 0ull;
+        } else {
+            S.pass = -1;
+            if (!refine) {
+                kt_result &o = out[m];
+                for (int i = 0; i < 3; ++i) o.mean[i] = s_mean[i];
+                for (int i = 0; i < 9; ++i) o.covariance[i] = cov[i];
+                o.response = clamped;
+                o.status = S.status;
+                o.pad_ = 0;
+            }
+        }
+    }
+    __syncthreads();
+    if (S.pass == pass + 1) {
+        unsigned long long *pm = posmax + (size_t)m * nxy * nxy;
+        for (int i = tid; i < nxy * nxy; i += KT_THREADS) pm[i] = 0ull;
+    }
+}
+
+// =================================================================================================
+// kt_fine_kernel: fine CorrelateScan + ComputeAngularCovariance, one workgroup per match
+// =================================================================================================
+__device__ __forceinline__ int kt_offset(const KtGeom &g, double cs, double sn, double2 l, double gox, double goy)
+{
+    const double ox = cs * l.x - sn * l.y;
+    const double oy = sn * l.x + cs * l.y;
+    return kt_w2g(ox + gox, gox, g.scale) + kt_w2g(oy + goy, goy, g.scale) * g.ws;
+}
+
+__global__ void __launch_bounds__(KT_THREADS)
+kt_fine_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict__ grids, int penalize,
+               kt_result *out)
+{
+    __shared__ unsigned scnt[KT_FINE_MAX_ANG][9];
+    __shared__ unsigned sred[4][9];
+    __shared__ double sresp[KT_FINE_MAX_ANG * 9];
+    __shared__ double s_mean[3];
+    __shared__ double s_best;
+    __shared__ int s_gi;
+    const int m = blockIdx.x;
+    KtState &S = st[m];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const double cx = S.mean[0], cy = S.mean[1], ch = S.mean[2];  // rSearchCenter = coarse rMean
+    const double gox = S.gox, goy = S.goy;
+    const int q = S.query, npts = S.npts;
+    const double2 *loc = P.loc + (size_t)q * g.n;
+    const unsigned char *bad = P.bad + (size_t)q * g.n;
+    const unsigned char *grid = grids + (size_t)m * g.grid_stride;
+    const unsigned ds = (unsigned)g.data_size;
+    const int nA = g.fnang;
+    const double startX = -g.foff;
+    const double astart = ch - g.faoff;
+    int err = 0;
+    int gpos[9];
+#pragma unroll
+    for (int p = 0; p < 9; ++p) {
+        const int ix = p % 3, iy = p / 3;
+        const double x = startX + (double)(uint32_t)ix * g.res;
+        const double y = startX + (double)(uint32_t)iy * g.res;
+        const int gx = kt_w2g(cx + x, gox, g.scale) + g.border, gy = kt_w2g(cy + y, goy, g.scale) + g.border;
+        if (gx < 0 || gx >= g.width || gy < 0 || gy >= g.height) err = 1;
+        gpos[p] = gx + gy * g.ws;
+    }
+    for (int a = 0; a < nA; ++a) {
+        const double angle = astart + (double)(uint32_t)a * g.fares;
+        const double cs = sdm_cos(angle), sn = sdm_sin(angle);
+        unsigned c[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = tid; k < npts; k += KT_THREADS) {
+            if (bad[k]) continue;
+            const int o = kt_offset(g, cs, sn, loc[k], gox, goy);
+#pragma unroll
+            for (int p = 0; p < 9; ++p) {
+                const int idx = gpos[p] + o;
+                if ((unsigned)idx < ds) c[p] += grid[idx];
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 9; ++p) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) c[p] += __shfl_xor(c[p], off, 64);
+            if (lane == 0) sred[wave][p] = c[p];
+        }
+        __syncthreads();
+        if (tid < 9) scnt[a][tid] = sred[0][tid] + sred[1][tid] + sred[2][tid] + sred[3][tid];
+        __syncthreads();
+    }
+    // responses in pose order (y, x, angle)
+    const int np = 9 * nA;
+    for (int i = tid; i < np; i += KT_THREADS) {
+        const int a = i % nA, p = i / nA;
+        double response = 0.0;
+        if (npts > 0) response = (double)scnt[a][p] / (double)(uint32_t)(npts * KT_OCC);
+        if (penalize && !kt_deq(response, 0.0)) {
+            const double x = startX + (double)(uint32_t)(p % 3) * g.res;
+            const double y = startX + (double)(uint32_t)(p / 3) * g.res;
+            const double sqd = kt_sq(x) + kt_sq(y);
+            double dp = 1.0 - (KT_GAIN * sqd / g.dvp);
+            dp = kt_max(dp, g.mdp);
+            const double angle = astart + (double)(uint32_t)a * g.fares;
+            const double sqa = kt_sq(angle - ch);
+            double ap = 1.0 - (KT_GAIN * sqa / g.avp);
+            ap = kt_max(ap, g.map_);
+            response *= (dp * ap);
+        }
+        sresp[i] = response;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double best = -1;
+        for (int i = 0; i < np; ++i) best = kt_max(best, sresp[i]);
+        double ax = 0.0, ay = 0.0, tx = 0.0, ty = 0.0;
+        int nt = 0;
+        for (int i = 0; i < np; ++i) {
+            if (!kt_deq(sresp[i], best)) continue;
+            const int a = i % nA, p = i / nA;
+            ax += cx + (startX + (double)(uint32_t)(p % 3) * g.res);
+            ay += cy + (startX + (double)(uint32_t)(p / 3) * g.res);
+            const double h = kt_norm_angle(astart + (double)(uint32_t)a * g.fares);
+            tx += sdm_cos(h);
+            ty += sdm_sin(h);
+            ++nt;
+        }
+        ax /= nt;
+        ay /= nt;
+        tx /= nt;
+        ty /= nt;
+        s_mean[0] = ax;
+        s_mean[1] = ay;
+        s_mean[2] = sdm_atan2(ty, tx);
+        s_best = best;
+        const int gx = kt_w2g(ax, gox, g.scale) + g.border, gy = kt_w2g(ay, goy, g.scale) + g.border;
+        if (gx < 0 || gx >= g.width || gy < 0 || gy >= g.height) {
+            err = 1;
+            s_gi = 0;
+        } else {
+            s_gi = gx + gy * g.ws;
+        }
+    }
+    __syncthreads();
+    // ComputeAngularCovariance: GetResponse at the best pose for every fine angle
+    const int gi = s_gi;
+    for (int a = 0; a < nA; ++a) {
+        const double angle = astart + (double)(uint32_t)a * g.fares;
+        const double cs = sdm_cos(angle), sn = sdm_sin(angle);
+        unsigned c = 0;
+        for (int k = tid; k < npts; k += KT_THREADS) {
+            if (bad[k]) continue;
+            const int idx = gi + kt_offset(g, cs, sn, loc[k], gox, goy);
+            if ((unsigned)idx < ds) c += grid[idx];
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+        if (lane == 0) sred[wave][0] = c;
+        __syncthreads();
+        if (tid == 0) scnt[a][0] = sred[0][0] + sred[1][0] + sred[2][0] + sred[3][0];
+        __syncthreads();
+    }
+    if (err) S.status = KT_ERANGE;
+    __syncthreads();
+    if (tid == 0) {
+        const double best = s_best;
+        const double best_angle = kt_norm_angle_diff(s_mean[2], ch);
+        double norm = 0.0, acc = 0.0;
+        for (int a = 0; a < nA; ++a) {
+            const double angle = astart + (double)(uint32_t)a * g.fares;
+            const double response = npts > 0 ? (double)scnt[a][0] / (double)(uint32_t)(npts * KT_OCC) : 0.0;
+            if (response >= (best - 0.1)) {
+                norm += response;
+                acc += (kt_sq(angle - best_angle) * response);
+            }
+        }
+        if (norm > KT_TOL) {
+            if (acc < KT_TOL) acc = kt_sq(g.fares);
+            acc /= norm;
+        } else {
+            acc = 1000 * kt_sq(g.fares);
+        }
+        kt_result &o = out[m];
+        for (int i = 0; i < 3; ++i) o.mean[i] = s_mean[i];
+        for (int i = 0; i < 9; ++i) o.covariance[i] = S.cov[i];
+        o.covariance[8] = acc;
+        o.response = best > 1.0 ? 1.0 : best;
+        o.status = S.status;
+        o.pad_ = 0;
+    }
+}
+
+}  // namespace s2d

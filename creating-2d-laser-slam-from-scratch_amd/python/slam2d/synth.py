@@ -147,3 +147,46 @@ def make_streams(num_streams: int, num_scans: int, seed: int = 12345, n_beams: i
         points = np.zeros((0,), np.float32)
         counts = np.zeros((0,), np.int32)
     return ScanSet(points=points, counts=counts, ranges=ranges, gt=gt)
+
+
+def karto_sequential(num_matches: int, num_base: int, seed: int = 777, perturb=(0.03, 0.03, 0.02),
+                     noise: float = 0.01, step: int = 2, phase: float = 0.3, n_beams: int = N_BEAMS):
+    """Karto sequential-matcher workload: T = num_matches + num_base scans along the
+    loop, `step` trajectory samples apart; scan i >= num_base is matched against the num_base scans
+    before it (the running scans, Mapper.cpp:2040).  Base scans carry their true poses (already
+    corrected by the mapper), the query an odometry pose = truth + N(0, perturb).
+    Returns (ranges [T, n_beams] with inf for no return, true poses [T, 3], query poses [T, 3])."""
+    rng = np.random.default_rng(seed)
+    T = num_matches + num_base
+    poses = trajectory(T * step, phase)[::step]
+    R = cast_ranges(poses, world_segments(), n_beams)
+    R = R + rng.normal(0.0, noise, R.shape)
+    qp = poses + rng.normal(0.0, 1.0, poses.shape) * np.asarray(perturb, np.float64)
+    return R, poses, qp
+
+
+def karto_loop(num_matches: int, chain: int = 10, seed: int = 778, perturb=(0.4, 0.4, 0.05), noise: float = 0.01,
+               n_beams: int = N_BEAMS):
+    """Loop-closure candidate batch (MapperGraph::TryCloseLoop, Mapper.cpp:976-1016): each query scan
+    (second lap) is matched against a chain of `chain` scans recorded near the same place on the first
+    lap; the query pose carries an accumulated drift ~ N(0, perturb).
+    Returns (query ranges [M, n], query poses [M, 3], true query poses [M, 3],
+             chain ranges [M, chain, n], chain poses [M, chain, 3])."""
+    rng = np.random.default_rng(seed)
+    segs = world_segments()
+    lap = 2.0 * math.pi
+    t0 = rng.uniform(0.0, lap, num_matches)
+    dt = 0.08 / 6.7
+    qt = t0 + lap + rng.uniform(-2 * dt, 2 * dt, num_matches)
+
+    def pose_at(t):
+        return np.stack([8.0 * np.cos(t), 5.0 * np.sin(t), np.arctan2(5.0 * np.cos(t), -8.0 * np.sin(t))], axis=-1)
+
+    qtrue = pose_at(qt)
+    ct = t0[:, None] + dt * 3 * (np.arange(chain)[None, :] - chain // 2)
+    cposes = pose_at(ct)
+    QR = cast_ranges(qtrue, segs, n_beams) + rng.normal(0.0, noise, (num_matches, n_beams))
+    CR = cast_ranges(cposes.reshape(-1, 3), segs, n_beams).reshape(num_matches, chain, n_beams)
+    CR = CR + rng.normal(0.0, noise, CR.shape)
+    qpose = qtrue + rng.normal(0.0, 1.0, qtrue.shape) * np.asarray(perturb, np.float64)
+    return QR, qpose, qtrue, CR, cposes

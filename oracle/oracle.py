@@ -333,3 +333,79 @@ def plicp(ref, sens, angle_min, angle_inc, first_guess=(0.0, 0.0, 0.0), params=N
     ok = L.plo_icp(C.byref(p), ref.shape[0], float(angle_min), float(angle_inc), _fp(ref), _fp(sens), _fp(g),
                    reduce_threads, _fp(x), C.byref(it), C.byref(nv), C.byref(err), _fp(hashes))
     return dict(x=x, valid=bool(ok), iterations=it.value, nvalid=nv.value, error=err.value)
+
+
+# ---------------------------------------------------------------------------------------------- Karto
+class KtLaser(C.Structure):
+    """ko_laser / kt_laser: the LaserRangeFinder fields LocalizedRangeScan::Update reads."""
+    _fields_ = [("minimum_angle", C.c_double), ("angular_resolution", C.c_double),
+                ("minimum_range", C.c_double), ("range_threshold", C.c_double),
+                ("n_readings", C.c_int), ("pad_", C.c_int)]
+
+
+class KtParams(C.Structure):
+    """ko_params / kt_params: one ScanMatcher's parameters (Mapper.cpp:1569-1660 names)."""
+    _fields_ = [("search_size", C.c_double), ("resolution", C.c_double), ("smear_deviation", C.c_double),
+                ("distance_variance_penalty", C.c_double), ("angle_variance_penalty", C.c_double),
+                ("fine_search_angle_offset", C.c_double), ("coarse_search_angle_offset", C.c_double),
+                ("coarse_angle_resolution", C.c_double), ("minimum_angle_penalty", C.c_double),
+                ("minimum_distance_penalty", C.c_double), ("use_response_expansion", C.c_int),
+                ("pad_", C.c_int)]
+
+
+_KO = None
+
+
+def karto_lib():
+    global _KO
+    if _KO is None:
+        L = _lib(os.path.join(BUILD, "libkarto_oracle.so"))
+        L.ko_match_scan.restype = _i
+        L.ko_match_scan.argtypes = [C.POINTER(KtLaser), C.POINTER(KtParams), _p, _p, _i, _p, _p, _i, _i, _p, _p,
+                                    C.POINTER(C.c_double)]
+        L.ko_grid_info.restype = _i
+        L.ko_grid_info.argtypes = [C.POINTER(KtParams), C.POINTER(KtLaser), _p]
+        L.ko_kernel.restype = _i
+        L.ko_kernel.argtypes = [C.POINTER(KtParams), C.POINTER(KtLaser), _p, _i]
+        L.ko_build_grid.restype = _i
+        L.ko_build_grid.argtypes = [C.POINTER(KtLaser), C.POINTER(KtParams), _p, _i, _p, _p, _p]
+        _KO = L
+    return _KO
+
+
+def karto_grid_info(params: KtParams, laser: KtLaser) -> dict:
+    out = np.zeros(10, np.int32)
+    rc = karto_lib().ko_grid_info(C.byref(params), C.byref(laser), _fp(out))
+    if rc:
+        raise ValueError(f"ko_grid_info: {rc}")
+    keys = ["grid_size", "border", "width", "ws", "data_size", "side", "probs_ws", "half", "ksize"]
+    return {k: int(v) for k, v in zip(keys, out)}
+
+
+def karto_match(laser: KtLaser, params: KtParams, q_ranges, q_pose, b_ranges, b_poses, penalize=True,
+                refine=True):
+    """CPU restatement of ScanMatcher::MatchScan (parity unpinned).  Returns (mean[3], cov[3,3], response)."""
+    q = np.ascontiguousarray(q_ranges, np.float64)
+    qp = np.ascontiguousarray(q_pose, np.float64)
+    b = np.ascontiguousarray(b_ranges, np.float64).reshape(-1, laser.n_readings)
+    bp = np.ascontiguousarray(b_poses, np.float64).reshape(-1, 3)
+    mean = np.zeros(3, np.float64)
+    cov = np.zeros(9, np.float64)
+    r = C.c_double()
+    rc = karto_lib().ko_match_scan(C.byref(laser), C.byref(params), _fp(q), _fp(qp), b.shape[0], _fp(b), _fp(bp),
+                                   int(penalize), int(refine), _fp(mean), _fp(cov), C.byref(r))
+    if rc:
+        raise RuntimeError(f"ko_match_scan: {rc}")
+    return mean, cov.reshape(3, 3), r.value
+
+
+def karto_build_grid(laser: KtLaser, params: KtParams, q_pose, b_ranges, b_poses) -> np.ndarray:
+    info = karto_grid_info(params, laser)
+    out = np.zeros(info["data_size"], np.uint8)
+    b = np.ascontiguousarray(b_ranges, np.float64).reshape(-1, laser.n_readings)
+    bp = np.ascontiguousarray(b_poses, np.float64).reshape(-1, 3)
+    qp = np.ascontiguousarray(q_pose, np.float64)
+    rc = karto_lib().ko_build_grid(C.byref(laser), C.byref(params), _fp(qp), b.shape[0], _fp(b), _fp(bp), _fp(out))
+    if rc:
+        raise RuntimeError(f"ko_build_grid: {rc}")
+    return out.reshape(info["width"], info["ws"])

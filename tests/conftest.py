@@ -19,7 +19,7 @@ def pytest_configure(config):
 @pytest.fixture(scope="session", autouse=True)
 def _built_oracle():
     """Build the CPU checkers if they are missing (gcc is available on both machines)."""
-    need = [os.path.join(REPO, "oracle", "build", n) for n in ("libhector_oracle.so", "libgmapping_oracle.so", "libplicp_oracle.so", "libhector_oracle_O0.so")]
+    need = [os.path.join(REPO, "oracle", "build", n) for n in ("libhector_oracle.so", "libgmapping_oracle.so", "libplicp_oracle.so", "libhector_oracle_O0.so", "libkarto_oracle.so")]
     if not all(os.path.exists(p) for p in need):
         subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "oracle"])
     yield

@@ -3,7 +3,10 @@
 // device kt_create fails with KT_ENODEV (no CPU fallback).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -36,7 +39,7 @@ size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 enum { K_PREPARE, K_BEGIN, K_BUILD, K_COARSE, K_SELECT, K_FINE, K_CLEAR, K_NUM };
 const char *const k_names[K_NUM] = {"kt_prepare_kernel", "kt_begin_kernel", "kt_build_kernel", "kt_coarse_kernel",
-                                    "kt_select_kernel",  "kt_fine_kernel",  "kt_clear(kt_build_kernel)"};
+                                    "kt_select_kernel",  "kt_fine_kernel",  "kt_build_kernel<1> (clear)"};
 }  // namespace
 
 struct kt_ctx {
@@ -44,6 +47,10 @@ struct kt_ctx {
     kt_params params{};
     KtGeom g{};
     int max_matches = 0, max_scans = 0, max_base = 0;
+    int slots = 0;  // match slots resident at once (kt_run_batch chunk)
+    int build_per_match = 1;  // CAS AddScans: one workgroup per match (1) or per (match, base scan) (0)
+    int binned = 0;           // AddScans by kt_addscans_kernel (tile-binned, plain stores)
+    int *d_scratch = nullptr, *d_dirty = nullptr, *d_dirty_cnt = nullptr;
     double *d_ranges = nullptr, *d_poses = nullptr;
     int *d_npts = nullptr;
     double2 *d_pts = nullptr, *d_loc = nullptr;
@@ -112,6 +119,7 @@ int kt_geometry(const kt_laser &L, const kt_params &p, KtGeom &g, std::vector<un
     g.cres = 2 * g.res;
     g.nxy = (int)(uint32_t)(h_round(g.coff * 2.0 / g.cres) + 1);
     g.tiles = (g.nxy + KT_TILE - 1) / KT_TILE;
+    if (g.nxy > KT_MAX_NXY) return kfail(KT_EINVAL, "coarse search wider than 1024 positions");
     g.use_expansion = p.use_response_expansion ? 1 : 0;
     g.npass = g.use_expansion ? 4 : 1;
     g.cares = p.coarse_angle_resolution;
@@ -141,6 +149,9 @@ int kt_geometry(const kt_laser &L, const kt_params &p, KtGeom &g, std::vector<un
     if (mp > 2.0e8) return kfail(KT_EINVAL, "coarse search window larger than 2e8 poses");
     g.max_poses = (int)mp;
     g.grid_stride = align256((size_t)g.data_size + 64);
+    g.tiles_x = (g.ws + 63) / 64;
+    g.tiles_y = (g.height + 63) / 64;
+    g.ntiles = g.tiles_x * g.tiles_y;
     return KT_OK;
 }
 
@@ -184,16 +195,25 @@ int kt_prepare(kt_ctx *c, int first, int count, hipStream_t s)
     return KT_OK;
 }
 
-int kt_run_batch(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, const int *d_bidx, int penalize,
+int kt_run_chunk(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, const int *d_bidx, int penalize,
                  int refine, kt_result *d_res, hipStream_t s)
 {
     const KtGeom &g = c->g;
+    const int groups = (count + 7) / 8;
     KT_LAUNCH(K_BEGIN, kt_begin_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->pool(), d_query, c->d_state,
               c->d_posmax);
-    if (c->max_base > 0)
-        KT_LAUNCH(K_BUILD, kt_build_kernel, dim3(c->max_base, count), dim3(KT_THREADS), 0, s, g, c->pool(),
-                  c->d_state, d_bbeg, d_bidx, c->d_kernel, c->d_grids, 0);
-    const int groups = (count + 7) / 8;
+    if (c->max_base > 0) {
+        if (c->binned)
+            KT_LAUNCH(K_BUILD, kt_addscans_kernel, dim3(count), dim3(KT_AS_WAVES * 64), 0, s, g, c->pool(), c->d_state,
+                      d_bbeg, d_bidx, c->d_kernel, c->d_grids, c->d_scratch, (size_t)c->max_base * g.n, c->d_dirty,
+                      c->d_dirty_cnt);
+        else if (c->build_per_match)
+            KT_LAUNCH(K_BUILD, (kt_build_kernel<0, 8>), dim3(count), dim3(512), 0, s, g, c->pool(), c->d_state, d_bbeg,
+                      d_bidx, c->d_kernel, c->d_grids, count, c->max_base);
+        else
+            KT_LAUNCH(K_BUILD, (kt_build_kernel<0, 4>), dim3(groups * 8 * c->max_base), dim3(KT_THREADS), 0, s, g,
+                      c->pool(), c->d_state, d_bbeg, d_bidx, c->d_kernel, c->d_grids, count, c->max_base);
+    }
     for (int pass = 0; pass < g.npass; ++pass) {
         const long long blocks = (long long)groups * 8 * g.nang[pass] * g.tiles * g.tiles;
         if (blocks > 0x7fffffffLL) return kfail(KT_EINVAL, "coarse launch too large: lower the batch size");
@@ -205,9 +225,26 @@ int kt_run_batch(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, co
     if (refine)
         KT_LAUNCH(K_FINE, kt_fine_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->pool(), c->d_state, c->d_grids,
                   penalize, d_res);
-    if (c->max_base > 0)
-        KT_LAUNCH(K_CLEAR, kt_build_kernel, dim3(c->max_base, count), dim3(KT_THREADS), 0, s, g, c->pool(),
-                  c->d_state, d_bbeg, d_bidx, c->d_kernel, c->d_grids, 1);
+    if (c->max_base > 0 && c->binned)
+        KT_LAUNCH(K_CLEAR, kt_clear_tiles_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->d_grids, c->d_dirty,
+                  c->d_dirty_cnt);
+    else if (c->max_base > 0)
+        KT_LAUNCH(K_CLEAR, (kt_build_kernel<1, 4>), dim3(groups * 8 * c->max_base), dim3(KT_THREADS), 0, s, g,
+                  c->pool(), c->d_state, d_bbeg, d_bidx, c->d_kernel, c->d_grids, count, c->max_base);
+    return KT_OK;
+}
+
+// The batch runs in chunks of `slots` matches (default: all of them).  Smaller chunks keep a chunk's
+// grids cache-resident but were measured slower (the per-match select / fine workgroups are latency
+// bound and need the whole batch to fill the GPU); SLAM2D_KT_SLOTS caps the slot memory.
+int kt_run_batch(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, const int *d_bidx, int penalize,
+                 int refine, kt_result *d_res, hipStream_t s)
+{
+    for (int c0 = 0; c0 < count; c0 += c->slots) {
+        const int cnt = std::min(c->slots, count - c0);
+        const int rc = kt_run_chunk(c, cnt, d_query + c0, d_bbeg + c0, d_bidx, penalize, refine, d_res + c0, s);
+        if (rc != KT_OK) return rc;
+    }
     return KT_OK;
 }
 
@@ -252,7 +289,7 @@ int kt_destroy(kt_ctx *c)
     if (c->stream) hipStreamSynchronize(c->stream);
     void *bufs[] = {c->d_ranges, c->d_poses, c->d_npts,    c->d_pts,     c->d_loc,   c->d_bad,  c->d_evt,
                     c->d_grids,  c->d_kernel, c->d_state, c->d_resp,    c->d_posmax, c->d_tie_idx, c->d_tie_val,
-                    c->d_query,  c->d_bbeg,  c->d_bidx,    c->d_res};
+                    c->d_query,  c->d_bbeg,  c->d_bidx,    c->d_res, c->d_scratch, c->d_dirty, c->d_dirty_cnt};
     for (void *b : bufs) hipFree(b);
     for (auto &p : c->ev_free) {
         hipEventDestroy(p.first);
@@ -291,12 +328,21 @@ int kt_create(kt_ctx **out, const kt_laser *laser, const kt_params *params, int 
     c->max_matches = max_matches;
     c->max_scans = max_scans;
     c->max_base = max_base_per_match;
+    {
+        const char *env = getenv("SLAM2D_KT_SLOTS");
+        const int want = env ? atoi(env) : 0;  // default: the whole batch resident (measured fastest)
+        c->slots = std::max(1, std::min(max_matches, want > 0 ? want : max_matches));
+        const char *bpm = getenv("SLAM2D_KT_BUILD");
+        if (bpm && !strcmp(bpm, "per_base")) c->build_per_match = 0;
+        c->binned = g.ntiles <= KT_AS_MAX_TILES && max_base_per_match <= KT_AS_MAX_BASE &&
+                    !(bpm && (!strcmp(bpm, "per_base") || !strcmp(bpm, "cas")));
+    }
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         return kfail(KT_EHIP, "hipStreamCreate", e);
     }
-    const size_t S = (size_t)max_scans, n = (size_t)g.n, M = (size_t)max_matches;
+    const size_t S = (size_t)max_scans, n = (size_t)g.n, M = (size_t)c->slots;
     const size_t mp = (size_t)g.max_poses, npos = (size_t)g.nxy * g.nxy;
 #define KALLOC(ptr, bytes)                                             \
     if ((e = hipMalloc((void **)&(ptr), (bytes))) != hipSuccess) {     \
@@ -317,10 +363,15 @@ int kt_create(kt_ctx **out, const kt_laser *laser, const kt_params *params, int 
     KALLOC(c->d_posmax, sizeof(unsigned long long) * npos * M);
     KALLOC(c->d_tie_idx, sizeof(int) * mp * M);
     KALLOC(c->d_tie_val, sizeof(double4) * std::max(mp, npos) * M);
-    KALLOC(c->d_query, sizeof(int) * M);
-    KALLOC(c->d_bbeg, sizeof(int) * (M + 1));
-    KALLOC(c->d_bidx, sizeof(int) * std::max<size_t>(1, M * (size_t)max_base_per_match));
-    KALLOC(c->d_res, sizeof(kt_result) * M);
+    KALLOC(c->d_query, sizeof(int));
+    KALLOC(c->d_bbeg, sizeof(int) * 2);
+    KALLOC(c->d_bidx, sizeof(int) * std::max<size_t>(1, (size_t)max_base_per_match));
+    KALLOC(c->d_res, sizeof(kt_result));
+    if (c->binned) {
+        KALLOC(c->d_scratch, sizeof(int) * M * std::max<size_t>(1, (size_t)max_base_per_match) * n);
+        KALLOC(c->d_dirty, sizeof(int) * M * (size_t)g.ntiles);
+        KALLOC(c->d_dirty_cnt, sizeof(int) * M);
+    }
 #undef KALLOC
     {
         const size_t shm = (size_t)g.n * (sizeof(double2) + sizeof(int));
@@ -432,6 +483,16 @@ int kt_set_timing(kt_ctx *c, int enable)
     c->timing = enable != 0;
     return KT_OK;
 }
+
+#if defined(KT_DIAG_STAMPS)
+// diagnostic builds only: per-workgroup s_memtime stamps of kt_addscans_kernel (8 per block)
+int kt_diag_stamps(unsigned long long *out, int blocks)
+{
+    KCHK(hipDeviceSynchronize());
+    KCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(kt_diag), sizeof(unsigned long long) * 8 * blocks));
+    return KT_OK;
+}
+#endif
 
 int kt_num_kernels(void) { return K_NUM; }
 const char *kt_kernel_name(int i) { return (i >= 0 && i < K_NUM) ? k_names[i] : ""; }

@@ -11,7 +11,8 @@
 //   kt_begin_kernel    per match: centre the correlation grid on the query's pose (MatchScan 1-4).
 //   kt_build_kernel    per (match, base scan): the viewpoint test of FindValidPoints, then AddScan +
 //                      SmearPoint (Mapper.cpp:716-748, Mapper.h:971-1005) as a byte-wise max of the
-//                      smear kernel into the grid (32-bit compare-and-swap words).  Order-free because
+//                      smear kernel: chunks of 16 consecutive points rendered in an LDS tile, merged
+//                      into the grid by 64-bit compare-and-swap per non-zero qword.  Order-free because
 //                      the kernel's only 100 is its centre (checked at kt_create).
 //   kt_coarse_kernel   per (match, angle, 16x16 position tile): GridIndexLookup::ComputeOffsets for one
 //                      angle into LDS (Karto.h:6455-6501), then GetResponse (Mapper.cpp:819-856) for the
@@ -25,8 +26,8 @@
 //                      covariance (Mapper.cpp:535-626), response expansion (Mapper.cpp:244-271).
 //   kt_fine_kernel     per match: the fine CorrelateScan (3x3 positions x fine angles) and
 //                      ComputeAngularCovariance (Mapper.cpp:638-690) in one workgroup.
-//   kt_build_kernel    again with clear = 1: zero exactly the words the smear touched, so the slot's
-//                      grid is clean for the next match without a 6 MB memset.
+//   kt_build_kernel    again with clear = 1: zero the chunks' footprint boxes, so the slot's grid is
+//                      clean for the next match without a 6 MB memset.
 // All arithmetic is double, with -ffp-contract=off and the deterministic sin / cos / atan2 of
 // detmath.h; the CPU restatement oracle/karto_oracle.c evaluates the same sequence (bit-exact parity).
 #include <hip/hip_runtime.h>
@@ -43,6 +44,8 @@ constexpr int KT_THREADS = 256;
 constexpr int KT_MAX_READINGS = 4096;
 constexpr int KT_TILE = 16;
 constexpr int KT_FINE_MAX_ANG = 64;
+constexpr int KT_MAX_NXY = 1024;  // coarse positions per axis
+constexpr int KT_SEL_ITEMS = 16;
 constexpr int KT_INVALID = INT_MIN;  // INVALID_SCAN: any position index + this is negative -> skipped
 constexpr double KT_PI = 3.14159265358979323846;
 constexpr double KT_2PI = 6.28318530717958647692;
@@ -71,6 +74,7 @@ struct KtGeom {
     int use_expansion;
     int max_poses;
     size_t grid_stride;                // bytes per match slot grid
+    int tiles_x, tiles_y, ntiles;      // 64 x 64-cell tiles of the grid (kt_addscans_kernel)
 };
 
 struct KtPool {
@@ -286,76 +290,487 @@ kt_begin_kernel(KtGeom g, KtPool P, const int *__restrict__ query, KtState *st, 
 
 // =================================================================================================
 // kt_build_kernel: AddScans (clear = 0) / zero the same footprints (clear = 1)
+//
+// Every wave takes chunks of KT_CHUNK consecutive points of one base scan (consecutive readings land
+// next to each other, so their smear footprints overlap heavily).  A chunk whose footprint bounding
+// box fits the wave's LDS tile is rendered there first (byte max, points in turn, lanes over the
+// kernel cells), then every non-zero word of the tile is merged into the grid with one 32-bit
+// compare-and-swap (first tried against 0: most words are fresh).  Chunks that do not fit (a jump
+// between walls) smear their points straight into the grid.  clear = 1 zeroes the chunk's whole
+// bounding box (every non-zero cell of the grid lies in some footprint, so the grid ends all-zero).
 // =================================================================================================
-__device__ __forceinline__ unsigned kt_bytemax4(unsigned a, unsigned b)
+constexpr int KT_CHUNK = 16;
+constexpr int KT_BT_W = 12;   // LDS tile: 12 qwords (96 cells) wide
+constexpr int KT_BT_H = 96;   // ... 96 rows tall
+constexpr int KT_FAST_KS = 15;  // kernels up to 15x15 (<= 4 cells per lane) use per-lane cell tables
+
+__device__ __forceinline__ unsigned long long kt_bytemax8(unsigned long long a, unsigned long long b)
 {
-    unsigned r = 0;
+    unsigned long long r = 0;
 #pragma unroll
-    for (int t = 0; t < 32; t += 8) r |= max((a >> t) & 0xFFu, (b >> t) & 0xFFu) << t;
+    for (int t = 0; t < 64; t += 8) r |= (unsigned long long)max((unsigned)(a >> t) & 0xFFu, (unsigned)(b >> t) & 0xFFu) << t;
     return r;
 }
 
-__global__ void __launch_bounds__(KT_THREADS)
+// Render the footprints of the points in `gmask` into the wave's LDS tile and merge the tile into the
+// grid (clear: zero the footprints' box).  False when their box does not fit the tile.
+__device__ __forceinline__ bool kt_group(unsigned long long gmask, bool ok, int cx, int cy, int lane, int h, int ks,
+                                         int wsw, unsigned long long *gw, unsigned long long *tile, const unsigned char *sk,
+                                         const int *cell_off, const int *cell_off2, const unsigned char *cell_kv,
+                                         int clear)
+{
+    const bool in = ok && ((gmask >> lane) & 1ull);
+    int x0 = in ? cx : INT_MAX, x1 = in ? cx : INT_MIN, y0 = in ? cy : INT_MAX, y1 = in ? cy : INT_MIN;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        x0 = min(x0, __shfl_xor(x0, off, 64));
+        x1 = max(x1, __shfl_xor(x1, off, 64));
+        y0 = min(y0, __shfl_xor(y0, off, 64));
+        y1 = max(y1, __shfl_xor(y1, off, 64));
+    }
+    const int bx0 = (x0 - h) & ~7, by0 = y0 - h;
+    const int ww = ((x1 + h) - bx0) / 8 + 1, hh = (y1 + h) - by0 + 1;
+    if (ww > KT_BT_W || hh > KT_BT_H) return false;
+    const int wbase = by0 * wsw + (bx0 >> 3);
+    const int nw = ww * hh;
+    if (clear) {
+        for (int t = lane; t < nw; t += 64) {
+            const int r = t / ww, q = t - r * ww;
+            gw[wbase + r * wsw + q] = 0ull;
+        }
+        return true;
+    }
+    unsigned char *tileb = reinterpret_cast<unsigned char *>(tile);
+    for (int t = lane; t < nw; t += 64) tile[t] = 0ull;
+    unsigned long long mm = gmask & __ballot(ok);
+    if (ks <= KT_FAST_KS) {
+        while (mm) {  // points in turn; every lane owns the same <= 4 kernel cells for each point
+            const int src = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            const int pbase = (__shfl(cy, src, 64) - h - by0) * (ww * 8) + (__shfl(cx, src, 64) - h - bx0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (cell_kv[u] == 0) continue;
+                unsigned char *cell = tileb + pbase + cell_off[u] * (ww * 8) + cell_off2[u];
+                if (cell_kv[u] > *cell) *cell = cell_kv[u];
+            }
+        }
+    } else {
+        while (mm) {
+            const int src = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            const int px = __shfl(cx, src, 64) - h - bx0, py = __shfl(cy, src, 64) - h - by0;
+            for (int t = lane; t < ks * ks; t += 64) {
+                const int jj = t / ks, ii = t - jj * ks;
+                const unsigned char kv = sk[ii + ks * jj];
+                unsigned char *cell = tileb + (py + jj) * (ww * 8) + (px + ii);
+                if (kv > *cell) *cell = kv;
+            }
+        }
+    }
+    // merge: 8 64-bit compare-and-swaps in flight per lane (a fresh word finishes in one), then the words that
+    // already held data
+#if defined(KT_DIAG_NOMERGE)
+    if (nw > 0) return true;
+#endif
+    for (int t0 = lane; t0 < nw; t0 += 64 * 8) {
+        unsigned long long want[8], old[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = t0 + 64 * u;
+            want[u] = t < nw ? tile[t] : 0ull;
+            old[u] = 0ull;
+            if (want[u] != 0ull) {
+                const int r = t / ww, q = t - r * ww;
+#if defined(KT_DIAG_STORE)
+                gw[wbase + r * wsw + q] = want[u];
+#else
+                old[u] = atomicCAS(gw + wbase + r * wsw + q, 0ull, want[u]);
+#endif
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (old[u] == 0ull) continue;
+            const int t = t0 + 64 * u;
+            const int r = t / ww, q = t - r * ww;
+            unsigned long long *w = gw + wbase + r * wsw + q;
+            unsigned long long o = old[u];
+            while (true) {
+                const unsigned long long nv = kt_bytemax8(o, want[u]);
+                if (nv == o) break;
+                const unsigned long long prev = atomicCAS(w, o, nv);
+                if (prev == o) break;
+                o = prev;
+            }
+        }
+    }
+    return true;
+}
+
+template <int clear, int WAVES>
+__global__ void __launch_bounds__(WAVES * 64)
 kt_build_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int *__restrict__ bbeg,
-                const int *__restrict__ bidx, const unsigned char *__restrict__ kernel, unsigned char *grids, int clear)
+                const int *__restrict__ bidx, const unsigned char *__restrict__ kernel, unsigned char *grids, int count,
+                int max_base)
 {
     __shared__ unsigned char sk[41 * 41];
-    const int m = blockIdx.y;
-    const int j = blockIdx.x;
-    const int b0 = bbeg[m], b1 = bbeg[m + 1];
-    if (b0 + j >= b1) return;
-    const int s = bidx[b0 + j];
-    for (int i = threadIdx.x; i < g.ksize * g.ksize; i += KT_THREADS) sk[i] = kernel[i];
+    __shared__ unsigned long long stile[WAVES][KT_BT_H * KT_BT_W];
+    // WAVES == 4: one workgroup per (match, base scan), XCD-aware (every block of match m on XCD m % 8);
+    // otherwise one workgroup per match whose waves share out all (base scan, chunk) pairs, so the
+    // overlapping chunks of different base scans rarely race for the same grid words.
+    int m, jlo, jhi;
+    if (WAVES == 4) {
+        const int b = blockIdx.x;
+        const int xcd = b & 7, q8 = b >> 3;
+        const int grp = q8 / max_base, j = q8 - grp * max_base;
+        m = grp * 8 + xcd;
+        if (m >= count) return;
+        jlo = bbeg[m] + j;
+        jhi = jlo + 1;
+        if (jlo >= bbeg[m + 1]) return;
+    } else {
+        m = blockIdx.x;
+        jlo = bbeg[m];
+        jhi = bbeg[m + 1];
+    }
+    for (int i = threadIdx.x; i < g.ksize * g.ksize; i += WAVES * 64) sk[i] = kernel[i];
     __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const KtState &S = st[m];
     const double vx = S.center[0], vy = S.center[1];
     const double gox = S.gox, goy = S.goy;
-    const int npts = P.npts[s];
-    const double2 *pts = P.pts + (size_t)s * g.n;
-    const int2 *evt = P.evt + (size_t)s * g.n;
     unsigned char *grid = grids + (size_t)m * g.grid_stride;
-    unsigned *gw = reinterpret_cast<unsigned *>(grid);
+    unsigned long long *gw = reinterpret_cast<unsigned long long *>(grid);
+    const int wsw = g.ws >> 3;  // qwords per grid row (ws is a multiple of 8)
     const int h = g.half, ks = g.ksize;
-    for (int k = threadIdx.x; k < npts; k += KT_THREADS) {
-        const int2 e = evt[k];
-        if (e.x < 0) continue;
-        const double2 f = pts[e.y], c = pts[e.x];
-        const double a = vy - f.y;
-        const double b = f.x - vx;
-        const double cc = f.y * vx - f.x * vy;
-        const double ss = c.x * a + c.y * b + cc;
-        if (ss < 0.0) continue;  // wrong side of the viewpoint (Mapper.cpp:795-799)
-        const double2 p = pts[k];
-        const int gx = kt_w2g(p.x, gox, g.scale), gy = kt_w2g(p.y, goy, g.scale);
-        if (!(gx >= 0 && gx < g.grid_size) || !(gy >= 0 && gy < g.grid_size)) continue;
-        const int cx = gx + g.border, cy = gy + g.border;
-        if (!clear && grid[cx + cy * g.ws] == KT_OCC) continue;  // value already set (Mapper.cpp:735-739)
-        for (int jj = -h; jj <= h; ++jj) {
-            const int row = (cx - h) + (cy + jj) * g.ws;  // first footprint byte of this row
-            const unsigned char *krow = sk + ks * (jj + h);
-            const int w0 = row >> 2, w1 = (row + ks - 1) >> 2;
-            for (int w = w0; w <= w1; ++w) {
-                if (clear) {
-                    gw[w] = 0u;
-                    continue;
-                }
-                unsigned want = 0;
+    unsigned long long *tile = stile[wave];
+    int cell_off[4], cell_off2[4];
+    unsigned char cell_kv[4];
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int col = w * 4 + t - row;
-                    if (col >= 0 && col < ks) want |= (unsigned)krow[col] << (8 * t);
-                }
-                if (want == 0u) continue;
-                unsigned old = gw[w];
-                while (true) {
-                    const unsigned nv = kt_bytemax4(old, want);
-                    if (nv == old) break;
-                    const unsigned prev = atomicCAS(gw + w, old, nv);
-                    if (prev == old) break;
-                    old = prev;
+    for (int u = 0; u < 4; ++u) {
+        const int t = lane + 64 * u;
+        const int jj = t / ks, ii = t - jj * ks;
+        const bool in = ks <= KT_FAST_KS && t < ks * ks;
+        cell_off[u] = in ? jj : 0;
+        cell_off2[u] = in ? ii : 0;
+        cell_kv[u] = in ? sk[ii + ks * jj] : 0;
+    }
+    const int cmax = (g.n + KT_CHUNK - 1) / KT_CHUNK;  // chunk slots per base scan
+    for (int id = wave; id < (jhi - jlo) * cmax; id += WAVES) {
+        const int jb = id / cmax, c = id - jb * cmax;
+        const int s = bidx[jlo + jb];
+        const int npts = P.npts[s];
+        if (c * KT_CHUNK >= npts) continue;
+        const double2 *pts = P.pts + (size_t)s * g.n;
+        const int2 *evt = P.evt + (size_t)s * g.n;
+        // ---- this chunk's points: FindValidPoints' viewpoint test, AddScan's ROI test ----
+        const int k = c * KT_CHUNK + lane;
+        bool ok = false;
+        int cx = 0, cy = 0;
+        if (lane < KT_CHUNK && k < npts) {
+            const int2 e = evt[k];
+            if (e.x >= 0) {
+                const double2 f = pts[e.y], cu = pts[e.x];
+                const double a = vy - f.y;
+                const double b = f.x - vx;
+                const double cc = f.y * vx - f.x * vy;
+                const double ss = cu.x * a + cu.y * b + cc;
+                if (!(ss < 0.0)) {  // wrong side of the viewpoint otherwise (Mapper.cpp:795-799)
+                    const double2 p = pts[k];
+                    const int gx = kt_w2g(p.x, gox, g.scale), gy = kt_w2g(p.y, goy, g.scale);
+                    if (gx >= 0 && gx < g.grid_size && gy >= 0 && gy < g.grid_size) {
+                        ok = true;
+                        cx = gx + g.border;
+                        cy = gy + g.border;
+                    }
                 }
             }
         }
+        const unsigned long long mask = __ballot(ok);
+        if (mask == 0ull) continue;
+        if (kt_group(mask, ok, cx, cy, lane, h, ks, wsw, gw, tile, sk, cell_off, cell_off2, cell_kv, clear)) continue;
+        // the chunk's box is too large (a jump between walls): quarters, then single points
+        for (int q = 0; q < KT_CHUNK; q += 4) {
+            const unsigned long long m4 = mask & (0xFull << q);
+            if (m4 == 0ull || kt_group(m4, ok, cx, cy, lane, h, ks, wsw, gw, tile, sk, cell_off, cell_off2, cell_kv, clear))
+                continue;
+            unsigned long long mm = m4;
+            while (mm) {  // one footprint always fits the tile (ks <= 41)
+                const int src = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                kt_group(1ull << src, ok, cx, cy, lane, h, ks, wsw, gw, tile, sk, cell_off, cell_off2, cell_kv, clear);
+            }
+        }
+    }
+}
+
+// =================================================================================================
+// kt_addscans_kernel: AddScans of one match per workgroup, binned by 64 x 64-cell grid tiles
+//
+// 1. every valid (FindValidPoints) in-ROI point of the match's base scans -> its cell, into a
+//    per-slot scratch list (all 512 threads: the dependent loads overlap across the breadth);
+// 2. passes over as many base scans as the LDS item store holds: count the points per tile their
+//    smear footprint overlaps, prefix, scatter the cells tile-sorted into LDS;
+// 3. every wave takes whole tiles: renders the tile's footprints into a 4 KB LDS tile (byte max,
+//    points in turn, lanes over kernel cells) and writes the tile with plain 8-byte stores -- the
+//    workgroup owns its match's grid, so no atomics touch global memory.  A tile written by an
+//    earlier pass is re-read first.  Written tiles are listed per slot for kt_clear_tiles_kernel.
+// =================================================================================================
+#if defined(KT_DIAG_STAMPS)
+__device__ unsigned long long kt_diag[65536 * 8];
+#define KT_STAMP(i) do { if (threadIdx.x == 0) kt_diag[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define KT_STAMP(i) do { } while (0)
+#endif
+constexpr int KT_AS_WAVES = 8;
+constexpr int KT_AS_ITEMS = 15360;     // tile-sorted footprint items per pass (60 KB of LDS)
+constexpr int KT_AS_MARGIN = 16;       // LDS tile margin (footprints of kernel half <= 8 stay inside)
+constexpr int KT_AS_TW = 64 + 2 * KT_AS_MARGIN;
+constexpr int KT_AS_MAX_TILES = 2048;  // tiles per grid (e.g. 2896 x 2896 cells)
+constexpr int KT_AS_MAX_BASE = 1024;
+
+template <int NW>
+__device__ __forceinline__ int kt_block_exscan_n(int v, int *sw, int *total)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += t;
+    }
+    if (lane == 63) sw[w] = inc;
+    __syncthreads();
+    int woff = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        woff += i < w ? sw[i] : 0;
+        tot += sw[i];
+    }
+    *total = tot;
+    __syncthreads();
+    return woff + inc - v;
+}
+
+__device__ __forceinline__ int kt_tiles_of(int cx, int cy, int h, int tiles_x, int *t)
+{
+    const int tx0 = (cx - h) >> 6, tx1 = (cx + h) >> 6, ty0 = (cy - h) >> 6, ty1 = (cy + h) >> 6;
+    int c = 0;
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) t[c++] = ty * tiles_x + tx;
+    return c;
+}
+
+__global__ void __launch_bounds__(KT_AS_WAVES * 64)
+kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int *__restrict__ bbeg,
+                   const int *__restrict__ bidx, const unsigned char *__restrict__ kernel, unsigned char *grids,
+                   int *scratch, size_t scratch_stride, int *dirty_list, int *dirty_count)
+{
+    __shared__ unsigned sitem[KT_AS_ITEMS];
+    __shared__ int soff[KT_AS_MAX_TILES + 1];
+    __shared__ int scur[KT_AS_MAX_TILES];
+    __shared__ unsigned char sdirty[KT_AS_MAX_TILES];
+    __shared__ int sscan[KT_AS_MAX_BASE];
+    __shared__ unsigned long long stile[KT_AS_WAVES][KT_AS_TW * KT_AS_TW / 8 + 8];  // + 64 trash bytes
+    __shared__ unsigned char sk[41 * 41];
+    __shared__ int sw[KT_AS_WAVES];
+    __shared__ int s_ndirty, s_pass_end;
+    constexpr int NT = KT_AS_WAVES * 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m = blockIdx.x;
+    const int jlo = bbeg[m], nb = bbeg[m + 1] - jlo;
+    const KtState &S = st[m];
+    const double vx = S.center[0], vy = S.center[1];
+    const double gox = S.gox, goy = S.goy;
+    const int n = g.n, h = g.half, ks = g.ksize, NTL = g.ntiles;
+    const int wsw = g.ws >> 3;
+    unsigned long long *gw = reinterpret_cast<unsigned long long *>(grids + (size_t)m * g.grid_stride);
+    int *cellv = scratch + (size_t)m * scratch_stride;
+    KT_STAMP(0);
+    for (int i = tid; i < ks * ks; i += NT) sk[i] = kernel[i];
+    for (int t = tid; t < NTL; t += NT) sdirty[t] = 0;
+    for (int j = tid; j < nb; j += NT) sscan[j] = 0;
+    if (tid == 0) s_ndirty = 0;
+    __syncthreads();
+    // ---- 1. cells of the valid in-ROI points ----
+    for (int i = tid; i < nb * n; i += NT) {
+        const int j = i / n, k = i - j * n;
+        const int s = bidx[jlo + j];
+        int cell = -1;
+        if (k < P.npts[s]) {
+            const double2 *pts = P.pts + (size_t)s * n;
+            const int2 e = P.evt[(size_t)s * n + k];
+            if (e.x >= 0) {
+                const double2 f = pts[e.y], cu = pts[e.x];
+                const double a = vy - f.y;
+                const double b = f.x - vx;
+                const double cc = f.y * vx - f.x * vy;
+                const double ss = cu.x * a + cu.y * b + cc;
+                if (!(ss < 0.0)) {  // wrong side of the viewpoint otherwise (Mapper.cpp:795-799)
+                    const double2 p = pts[k];
+                    const int gx = kt_w2g(p.x, gox, g.scale), gy = kt_w2g(p.y, goy, g.scale);
+                    if (gx >= 0 && gx < g.grid_size && gy >= 0 && gy < g.grid_size)
+                        cell = (gx + g.border) | ((gy + g.border) << 16);
+                }
+            }
+        }
+        cellv[i] = cell;
+        if (cell >= 0) {
+            int tl[4];
+            atomicAdd(&sscan[j], kt_tiles_of(cell & 0xFFFF, cell >> 16, h, g.tiles_x, tl));
+        }
+    }
+    __syncthreads();
+    KT_STAMP(1);
+    // per-lane kernel cells (ks <= 15: at most 4 of the <= 225 cells per lane)
+    int cell_dy[4], cell_dx[4];
+    unsigned char cell_kv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int t = lane + 64 * u;
+        const int jj = t / ks, ii = t - jj * ks;
+        const bool in = ks <= KT_FAST_KS && t < ks * ks;
+        cell_dy[u] = in ? jj : 0;
+        cell_dx[u] = in ? ii : 0;
+        cell_kv[u] = in ? sk[ii + ks * jj] : 0;
+    }
+    unsigned long long *tile = stile[wave];
+    unsigned char *tileb = reinterpret_cast<unsigned char *>(tile);
+    int pa = 0;
+    while (pa < nb) {
+        if (tid == 0) {  // as many base scans as the item store holds (one always fits: <= 4 * 4096)
+            int tot = 0, pb = pa;
+            while (pb < nb && tot + sscan[pb] <= KT_AS_ITEMS) tot += sscan[pb++];
+            s_pass_end = pb;
+        }
+        for (int t = tid; t < NTL; t += NT) scur[t] = 0;
+        __syncthreads();
+        const int pb = s_pass_end;
+        // ---- 2. count per tile, prefix, scatter tile-sorted ----
+        for (int i = pa * n + tid; i < pb * n; i += NT) {
+            const int cell = cellv[i];
+            if (cell < 0) continue;
+            int tl[4];
+            const int c = kt_tiles_of(cell & 0xFFFF, cell >> 16, h, g.tiles_x, tl);
+            for (int q = 0; q < c; ++q) atomicAdd(&scur[tl[q]], 1);
+        }
+        __syncthreads();
+        {
+            const int per = (NTL + NT - 1) / NT;
+            const int t0 = min(tid * per, NTL), t1 = min(t0 + per, NTL);
+            int loc = 0;
+            for (int t = t0; t < t1; ++t) loc += scur[t];
+            int tot;
+            int pre = kt_block_exscan_n<KT_AS_WAVES>(loc, sw, &tot);
+            for (int t = t0; t < t1; ++t) {
+                const int c = scur[t];
+                soff[t] = pre;
+                scur[t] = pre;
+                pre += c;
+            }
+            if (tid == 0) soff[NTL] = tot;
+        }
+        __syncthreads();
+        if (pa == 0) KT_STAMP(2);
+        for (int i = pa * n + tid; i < pb * n; i += NT) {
+            const int cell = cellv[i];
+            if (cell < 0) continue;
+            int tl[4];
+            const int c = kt_tiles_of(cell & 0xFFFF, cell >> 16, h, g.tiles_x, tl);
+            for (int q = 0; q < c; ++q) sitem[atomicAdd(&scur[tl[q]], 1)] = (unsigned)cell;
+        }
+        __syncthreads();
+        if (pa == 0) KT_STAMP(3);
+        // ---- 3. render whole tiles, plain stores ----
+        // The LDS tile is the 64 x 64 tile plus a 16-cell margin on every side, so a footprint of any
+        // point listed for the tile (kernel half <= 8 in this path) lies inside it: no bounds tests,
+        // no divergence; cells a lane does not own get max(x, 0) = x written back.
+        for (int t = wave; t < NTL; t += KT_AS_WAVES) {
+            const int c0 = soff[t], c1 = soff[t + 1];
+            if (c0 == c1) continue;
+            const int ty = t / g.tiles_x, tx = t - ty * g.tiles_x;
+            const int x0 = tx * 64, y0 = ty * 64;
+            const bool was = sdirty[t] != 0;
+            for (int q = lane; q < KT_AS_TW * KT_AS_TW / 8; q += 64) tile[q] = 0ull;
+            if (was)
+                for (int q = lane; q < 512; q += 64) {
+                    const int r = q >> 3, xq = (x0 >> 3) + (q & 7), y = y0 + r;
+                    if (y < g.height && xq < wsw)
+                        tile[((r + KT_AS_MARGIN) * KT_AS_TW + KT_AS_MARGIN) / 8 + (q & 7)] = gw[(size_t)y * wsw + xq];
+                }
+            if (ks <= KT_FAST_KS) {
+                // lanes that own no kernel cell in slot u work on a private trash byte, so no two lanes
+                // of one store ever address the same byte
+                int coff[4];
+                bool own[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    own[u] = lane + 64 * u < ks * ks;
+                    coff[u] = cell_dy[u] * KT_AS_TW + cell_dx[u];
+                }
+                const int trash = KT_AS_TW * KT_AS_TW + lane;
+                const int base = (KT_AS_MARGIN - h - y0) * KT_AS_TW + (KT_AS_MARGIN - h - x0);
+                for (int c = c0; c < c1; ++c) {
+                    const unsigned cell = sitem[c];
+                    const int o = base + (int)(cell >> 16) * KT_AS_TW + (int)(cell & 0xFFFFu);
+                    int ad[4];
+                    unsigned cur[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        ad[u] = own[u] ? o + coff[u] : trash;
+                        cur[u] = tileb[ad[u]];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) tileb[ad[u]] = (unsigned char)max(cur[u], (unsigned)cell_kv[u]);
+                }
+            } else {
+                for (int c = c0; c < c1; ++c) {
+                    const unsigned cell = sitem[c];
+                    const int bx = (int)(cell & 0xFFFFu) - h - x0, by = (int)(cell >> 16) - h - y0;
+                    for (int q = lane; q < ks * ks; q += 64) {
+                        const int jj = q / ks, ii = q - jj * ks;
+                        const int x = bx + ii, y = by + jj;
+                        if ((unsigned)x >= 64u || (unsigned)y >= 64u) continue;
+                        const unsigned char kv = sk[ii + ks * jj];
+                        unsigned char *b = tileb + (y + KT_AS_MARGIN) * KT_AS_TW + x + KT_AS_MARGIN;
+                        if (kv > *b) *b = kv;
+                    }
+                }
+            }
+            for (int q = lane; q < 512; q += 64) {
+                const int r = q >> 3, xq = (x0 >> 3) + (q & 7), y = y0 + r;
+                if (y < g.height && xq < wsw)
+                    gw[(size_t)y * wsw + xq] = tile[((r + KT_AS_MARGIN) * KT_AS_TW + KT_AS_MARGIN) / 8 + (q & 7)];
+            }
+            if (lane == 0 && !was) {
+                sdirty[t] = 1;
+                dirty_list[(size_t)m * NTL + atomicAdd(&s_ndirty, 1)] = t;
+            }
+        }
+        __syncthreads();
+        if (pa == 0) KT_STAMP(4);
+        pa = pb;
+    }
+    if (tid == 0) dirty_count[m] = s_ndirty;
+    KT_STAMP(5);
+}
+
+// zero every tile kt_addscans_kernel wrote for the slot
+__global__ void __launch_bounds__(KT_THREADS)
+kt_clear_tiles_kernel(KtGeom g, unsigned char *grids, const int *__restrict__ dirty_list,
+                      const int *__restrict__ dirty_count)
+{
+    const int m = blockIdx.x;
+    const int cnt = dirty_count[m];
+    const int wsw = g.ws >> 3;
+    unsigned long long *gw = reinterpret_cast<unsigned long long *>(grids + (size_t)m * g.grid_stride);
+    for (int i = threadIdx.x; i < cnt * 512; i += KT_THREADS) {
+        const int t = dirty_list[(size_t)m * g.ntiles + (i >> 9)];
+        const int q = i & 511;
+        const int ty = t / g.tiles_x, tx = t - ty * g.tiles_x;
+        const int y = ty * 64 + (q >> 3), xq = tx * 8 + (q & 7);
+        if (y < g.height && xq < wsw) gw[(size_t)y * wsw + xq] = 0ull;
     }
 }
 
@@ -521,6 +936,7 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
     __shared__ int s_n;
     __shared__ double s_mean[3];
     __shared__ int s_err;
+    __shared__ int s_pcx[KT_MAX_NXY], s_pcy[KT_MAX_NXY];
     const int m = blockIdx.x;
     KtState &S = st[m];
     if (S.pass != pass) return;
@@ -540,14 +956,27 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
         s_err = 0;
     }
     __syncthreads();
-    // poses with DoubleEqual(response, best), in pose order
-    for (int base = 0; base < np; base += KT_THREADS) {
-        const int i = base + tid;
-        const int f = (i < np && kt_deq(r[i], best)) ? 1 : 0;
+    // poses with DoubleEqual(response, best), in pose order (16 consecutive poses per thread and pass)
+    for (int base = 0; base < np; base += KT_THREADS * KT_SEL_ITEMS) {
+        const int i0 = base + tid * KT_SEL_ITEMS;
+        unsigned fl = 0;
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < KT_SEL_ITEMS; ++j) {
+            const int i = i0 + j;
+            if (i < np && kt_deq(r[i], best)) {
+                fl |= 1u << j;
+                ++c;
+            }
+        }
         int tot;
-        const int pre = kt_block_exscan(f, sw, &tot);
+        int pre = kt_block_exscan(c, sw, &tot);
         const int n0 = s_n;
-        if (f) ti[n0 + pre] = i;
+        while (fl) {
+            const int j = __builtin_ctz(fl);
+            fl &= fl - 1;
+            ti[n0 + pre++] = i0 + j;
+        }
         __syncthreads();
         if (tid == 0) s_n = n0 + tot;
         __syncthreads();
@@ -600,33 +1029,37 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
         if (tid == 0) s_n = 0;
         __syncthreads();
         const int npos = nxy * nxy;
+        // probability-grid cell of every coarse column / row (WorldToGrid of the pose positions)
+        for (int i = tid; i < nxy; i += KT_THREADS) {
+            const double v = startX + (double)(uint32_t)i * g.cres;
+            const int pgx = kt_w2g(cx + v, pgox, g.scale), pgy = kt_w2g(cy + v, pgoy, g.scale);
+            s_pcx[i] = pgx;
+            s_pcy[i] = pgy;
+            if (pgx < 0 || pgx >= g.side || pgy < 0 || pgy >= g.side)
+                s_err = 2;  // "Index out of range in probability search" (Mapper.cpp:446)
+        }
+        __syncthreads();
         for (int base = 0; base < npos; base += KT_THREADS) {
             const int i = base + tid;
             int f = 0;
             double val = 0.0;
             if (i < npos) {
                 const int ix = i % nxy, iy = i / nxy;
-                const double x = cx + (startX + (double)(uint32_t)ix * g.cres);
-                const double y = cy + (startX + (double)(uint32_t)iy * g.cres);
-                const int pgx = kt_w2g(x, pgox, g.scale), pgy = kt_w2g(y, pgoy, g.scale);
-                if (pgx < 0 || pgx >= g.side || pgy < 0 || pgy >= g.side) {
-                    s_err = 2;  // "Index out of range in probability search" (Mapper.cpp:446)
-                } else {
-                    // the probability cell holds the max over every pose that lands in it: this
-                    // position and any neighbour whose coordinates round to the same cell
-                    unsigned long long v = pm[i];
+                // the probability cell holds the max over every pose that lands in it: this position
+                // and any neighbour whose coordinates round to the same cell
+                const int px = s_pcx[ix], py = s_pcy[iy];
+                const bool xl = ix > 0 && s_pcx[ix - 1] == px, xr = ix + 1 < nxy && s_pcx[ix + 1] == px;
+                const bool yl = iy > 0 && s_pcy[iy - 1] == py, yr = iy + 1 < nxy && s_pcy[iy + 1] == py;
+                unsigned long long v = pm[i];
+                if (xl | xr | yl | yr) {
                     for (int dy = -1; dy <= 1; ++dy)
                         for (int dx = -1; dx <= 1; ++dx) {
-                            const int jx = ix + dx, jy = iy + dy;
-                            if ((dx == 0 && dy == 0) || jx < 0 || jy < 0 || jx >= nxy || jy >= nxy) continue;
-                            const double xx = cx + (startX + (double)(uint32_t)jx * g.cres);
-                            const double yy = cy + (startX + (double)(uint32_t)jy * g.cres);
-                            if (kt_w2g(xx, pgox, g.scale) == pgx && kt_w2g(yy, pgoy, g.scale) == pgy)
-                                v = max(v, pm[jy * nxy + jx]);
+                            if ((dx < 0 && !xl) || (dx > 0 && !xr) || (dy < 0 && !yl) || (dy > 0 && !yr)) continue;
+                            v = max(v, pm[(iy + dy) * nxy + ix + dx]);
                         }
-                    val = kt_dbl(v);
-                    f = val >= lo ? 1 : 0;
                 }
+                val = kt_dbl(v);
+                f = val >= lo ? 1 : 0;
             }
             int tot;
             const int pre = kt_block_exscan(f, sw, &tot);

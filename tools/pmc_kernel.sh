@@ -22,5 +22,5 @@ for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
         k = r["Kernel_Name"].split("(")[0].replace("s2d::", "")
         agg[(k, r["Counter_Name"])] += float(r["Counter_Value"]); cnt[(k, r["Counter_Name"])] += 1
 for (k, c), v in sorted(agg.items()):
-    if k.startswith("hs_"): print(f"{k:24s} {c:24s} {v/ max(cnt[(k,c)],1):18.0f} (per dispatch avg over {cnt[(k,c)]})")
+    if k.startswith(("hs_", "kt_", "gm_", "pl_")): print(f"{k:24s} {c:24s} {v/ max(cnt[(k,c)],1):18.0f} (per dispatch avg over {cnt[(k,c)]})")
 PY

@@ -36,7 +36,9 @@ def main():
     shutil.copyfile(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     with open(os.path.join(src, "bench_trace.json")) as f:
         bench = json.loads([ln for ln in f if ln.startswith("{")][-1])
-    cfg, streams = bench["config"]["config"], bench["config"]["streams_per_gpu"]
+    cfg = bench["config"]["config"]
+    streams = next((bench["config"][k] for k in ("streams_per_gpu", "matches_per_gpu", "pairs_per_gpu", "particles_per_gpu")
+                    if k in bench["config"]), None)
 
     dur = {}
     with open(stats) as f:
@@ -52,8 +54,8 @@ def main():
         for k, v in acc.items():
             pmc[k][ctr] = sum(v) / len(v)
 
-    lines = [f"# rocprofv3 summary `{tag}` ({cfg}, {streams} streams/GPU)", "",
-             f"bench line of the traced run: value {bench['value']} scans/s, ms/step {bench['ms_per_step']}", "",
+    lines = [f"# rocprofv3 summary `{tag}` ({cfg}, {streams} units/GPU)", "",
+             f"bench line of the traced run: value {bench['value']} {bench['unit']}, ms/step {bench['ms_per_step']}", "",
              "| kernel | calls | avg us | FETCH_SIZE KB | WRITE_SIZE KB | HBM bytes/launch (2F+W) | GB/s |",
              "|---|---|---|---|---|---|---|"]
     entries = []
@@ -63,7 +65,7 @@ def main():
         gbs = f"{tb / avg:.1f}" if tb else "-"
         lines.append(f"| {k} | {calls} | {avg / 1e3:.1f} | {fe if fe is not None else '-'} | "
                      f"{wr if wr is not None else '-'} | {tb if tb else '-'} | {gbs} |")
-        if tb and k.startswith("hs_"):
+        if tb and k.startswith(("hs_", "kt_", "gm_", "pl_")):
             entries.append({"kernel": k, "config": cfg, "streams": streams, "avg_ns": avg,
                             "fetch_kb": fe, "write_kb": wr, "traffic_bytes_per_launch": tb,
                             "source": f"profiles/{rnd}/{tag}_summary.md"})

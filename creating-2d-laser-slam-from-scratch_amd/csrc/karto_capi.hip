@@ -202,12 +202,15 @@ int kt_run_chunk(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, co
     const int groups = (count + 7) / 8;
     KT_LAUNCH(K_BEGIN, kt_begin_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->pool(), d_query, c->d_state,
               c->d_posmax);
+    // the binned AddScans runs one workgroup per match: small batches use the per-(match, base scan) kernel
+    const bool binned = c->binned && count >= 128;
+    const bool per_match = !binned && c->build_per_match && count >= 128;
     if (c->max_base > 0) {
-        if (c->binned)
+        if (binned)
             KT_LAUNCH(K_BUILD, kt_addscans_kernel, dim3(count), dim3(KT_AS_WAVES * 64), 0, s, g, c->pool(), c->d_state,
                       d_bbeg, d_bidx, c->d_kernel, c->d_grids, c->d_scratch, (size_t)c->max_base * g.n, c->d_dirty,
                       c->d_dirty_cnt);
-        else if (c->build_per_match)
+        else if (per_match)
             KT_LAUNCH(K_BUILD, (kt_build_kernel<0, 8>), dim3(count), dim3(512), 0, s, g, c->pool(), c->d_state, d_bbeg,
                       d_bidx, c->d_kernel, c->d_grids, count, c->max_base);
         else
@@ -225,7 +228,7 @@ int kt_run_chunk(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, co
     if (refine)
         KT_LAUNCH(K_FINE, kt_fine_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->pool(), c->d_state, c->d_grids,
                   penalize, d_res);
-    if (c->max_base > 0 && c->binned)
+    if (c->max_base > 0 && binned)
         KT_LAUNCH(K_CLEAR, kt_clear_tiles_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->d_grids, c->d_dirty,
                   c->d_dirty_cnt);
     else if (c->max_base > 0)

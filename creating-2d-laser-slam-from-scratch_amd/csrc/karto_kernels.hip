@@ -854,8 +854,44 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
     unsigned acc01 = 0, acc23 = 0;
     int since = 0;
     if (fast) {
+        // 8 points per iteration: 8 independent 8-byte gathers in flight per lane
         const int base = gpos[0];
-        for (int k = wave; k < npts; k += 4) {
+        int k = wave;
+        for (; k + 28 < npts; k += 32) {
+            int bi[8];
+            bool allin = true;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                bi[j] = base + soff[k + 4 * j];
+                allin = allin && (unsigned)bi[j] < lim;
+            }
+            if (allin) {
+                uint2 v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) __builtin_memcpy(&v[j], grid + bi[j], 8);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    acc01 += v[j].x & 0x00FF00FFu;
+                    acc23 += v[j].y & 0x00FF00FFu;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int b = bi[j];
+                    if ((unsigned)b < ds) c0 += grid[b];
+                    if ((unsigned)(b + 2) < ds) c1 += grid[b + 2];
+                    if ((unsigned)(b + 4) < ds) c2 += grid[b + 4];
+                    if ((unsigned)(b + 6) < ds) c3 += grid[b + 6];
+                }
+            }
+            since += 8;
+            if (since >= 504) {  // 512 * 100 < 65536: flush the packed 16-bit sums
+                c0 += acc01 & 0xFFFFu; c1 += acc01 >> 16; c2 += acc23 & 0xFFFFu; c3 += acc23 >> 16;
+                acc01 = acc23 = 0;
+                since = 0;
+            }
+        }
+        for (; k < npts; k += 4) {
             const int bi = base + soff[k];
             if ((unsigned)bi < lim) {
                 uint2 v;
@@ -867,11 +903,6 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
                 if ((unsigned)(bi + 2) < ds) c1 += grid[bi + 2];
                 if ((unsigned)(bi + 4) < ds) c2 += grid[bi + 4];
                 if ((unsigned)(bi + 6) < ds) c3 += grid[bi + 6];
-            }
-            if (++since == 512) {  // 512 * 100 < 65536: flush the packed 16-bit sums
-                c0 += acc01 & 0xFFFFu; c1 += acc01 >> 16; c2 += acc23 & 0xFFFFu; c3 += acc23 >> 16;
-                acc01 = acc23 = 0;
-                since = 0;
             }
         }
         c0 += acc01 & 0xFFFFu; c1 += acc01 >> 16; c2 += acc23 & 0xFFFFu; c3 += acc23 >> 16;
@@ -1181,10 +1212,17 @@ kt_fine_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict_
         for (int k = tid; k < npts; k += KT_THREADS) {
             if (bad[k]) continue;
             const int o = kt_offset(g, cs, sn, loc[k], gox, goy);
+            // branch-free: out-of-range cells read cell 0 and count 0, so all 9 gathers are in flight
+            unsigned char v[9];
 #pragma unroll
             for (int p = 0; p < 9; ++p) {
                 const int idx = gpos[p] + o;
-                if ((unsigned)idx < ds) c[p] += grid[idx];
+                v[p] = grid[(unsigned)idx < ds ? idx : 0];
+            }
+#pragma unroll
+            for (int p = 0; p < 9; ++p) {
+                const int idx = gpos[p] + o;
+                c[p] += (unsigned)idx < ds ? v[p] : 0u;
             }
         }
 #pragma unroll

@@ -96,13 +96,13 @@ def test_invalid_readings_and_clean_slots(gpu):
 
 
 def test_batch_device_matches_single(gpu):
-    """kt_match_batch_device over pooled scans: a batch of 24 sequential matches (ragged base counts)
+    """kt_match_batch_device over pooled scans: a batch of 136 sequential matches (ragged base counts)
     equals the oracle match by match."""
     import torch
 
     lz = _laser()
     p = karto.default_params()
-    M, B = 24, 8
+    M, B = 136, 8  # >= 128: the binned AddScans path
     R, T, Q = synth.karto_sequential(M, B, seed=9)
     S = R.shape[0]
     # pool: slots [0, S) true-pose scans (bases), [S, S + M) the queries at their odometry poses
@@ -136,3 +136,31 @@ def test_grid_matches_oracle_addscans(gpu):
     a = sm.MatchScan(R[10], Q[10], R[:10], T[:10])
     b = sm.MatchScan(R[10], Q[10], R[:10], T[:10])
     _same(a, b)
+
+
+def test_batch_device_loop_window(gpu):
+    """A loop-closure candidate batch (>= 128 matches: binned AddScans) on a wide coarse window
+    (21 x 21 positions: the 32 x 32-tile coarse kernel), doPenalize = doRefine = false as
+    TryCloseLoop's first call (Mapper.cpp:991-992)."""
+    import torch
+
+    lz = _laser()
+    p = karto.default_params(loop=True)
+    p.search_size = 2.0  # 41 x 41 probability grid, 21 x 21 coarse positions
+    M, K = 128, 6
+    QR, qp, qt, CR, CP = synth.karto_loop(M, K, seed=17, perturb=(0.2, 0.2, 0.03))
+    sm = karto.ScanMatcher(lz, p, max_matches=M, max_scans=M * (K + 1), max_base=K)
+    pr = torch.tensor(np.concatenate([QR, CR.reshape(-1, synth.N_BEAMS)]), dtype=torch.float64, device="cuda")
+    pp = torch.tensor(np.concatenate([qp, CP.reshape(-1, 3)]), dtype=torch.float64, device="cuda")
+    sm.set_scans_device(0, M * (K + 1), pr.data_ptr(), pp.data_ptr())
+    q = torch.arange(M, dtype=torch.int32, device="cuda")
+    beg = torch.arange(M + 1, dtype=torch.int32, device="cuda") * K
+    idx = torch.arange(M, M + M * K, dtype=torch.int32, device="cuda")
+    res = torch.zeros(M * C.sizeof(karto.KtResult), dtype=torch.uint8, device="cuda")
+    sm.match_batch_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), res.data_ptr(), False, False)
+    torch.cuda.synchronize()
+    out = karto.results_from_bytes(res.cpu().numpy())
+    for i in range(0, M, 7):
+        o = O.karto_match(_olaser(lz), _oparams(p), QR[i], qp[i], CR[i], CP[i], False, False)
+        assert out["status"][i] == 0
+        _same((out["mean"][i], out["covariance"][i].reshape(3, 3), out["response"][i]), o)

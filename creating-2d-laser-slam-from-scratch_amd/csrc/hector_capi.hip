@@ -195,7 +195,7 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     if (mode == MODE_MATCH_ONLY) return HS_OK;
     // hs_update_kernel keeps the scan's rays in LDS: beyond 64 KB of dynamic LDS (max_points > ~11k)
     // the binned kernels, whose LDS use is independent of the scan size, take over
-    const size_t upd_shmem = sizeof(unsigned) * (2 * (size_t)UPD_TILE_WORDS + (size_t)((c->max_points + 3) & ~3) +
+    const size_t upd_shmem = sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + (size_t)((c->max_points + 3) & ~3) +
                                                  4 * (size_t)((c->max_points + 63) / 64));
     if (c->update_single && upd_shmem <= 65536) {
         begin_timed(c, 2, s);
@@ -659,6 +659,9 @@ int hs_get_queue_stats(hs_ctx *c, int64_t out[8], int reset_stamps)
         out[3] += q[p].overflow;
     }
     for (int k = 0; k < 4; ++k) out[4 + k] = (int64_t)st[k];
+#ifdef S2D_VISITS
+    for (int k = 0; k < 4; ++k) out[k] = (int64_t)st[4 + k];  // diagnostic build: raster visit counters
+#endif
     if (reset_stamps) {
         memset(st, 0, sizeof(st));
         HCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), st, sizeof(st)));

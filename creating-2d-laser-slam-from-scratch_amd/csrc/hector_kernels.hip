@@ -1042,16 +1042,21 @@ constexpr int UPD_TILE_WORDS = UPD_TH * UPD_STRIDE;   // one LDS mark array
 static_assert(UPD_STRIDE % 4 == 0 && UPD_STRIDE >= TILE, "quad-aligned LDS rows");
 constexpr int UPD_QUADS = TILE * UPD_TH / 4 / UPD_THREADS;  // apply quads per thread per tile
 
-// bresenhamCellFree / bresenhamCellOcc outcome of one scan for one cell (h, f: first hitting /
-// freeing beam, W_NONE if none): GridMapLogOddsFunctions (GridMapLogOdds.h:108-129)
-__device__ __forceinline__ int apply_cell(float &l, int &u, unsigned h, unsigned f, float lf, float lo, int mf, int mo)
+// Tile marks: ONE LDS word per tile cell, lowered with blind atomicMin of a beam EVENT code
+//   free step of beam b -> 2b + 1,    end (hit) cell of beam b -> 2b,
+// plus one hit bit per cell.  The word ends as the earliest event at the cell in beam order (the
+// order updateByScan walks the beams).  A beam never frees its own end cell, so with the hit bit
+// set an odd word means a lower-index beam freed the cell before the first beam that hits it, an
+// even word that the hit came first -- all that bresenhamCellFree / bresenhamCellOcc (:302-330)
+// depend on within one scan.  GridMapLogOddsFunctions (GridMapLogOdds.h:108-129):
+__device__ __forceinline__ int apply_cell(float &l, int &u, unsigned m, unsigned hit, float lf, float lo, int mf, int mo)
 {
-    if ((h & f) == W_NONE) return 0;
-    if (h == W_NONE) {
+    if (m == W_NONE) return 0;
+    if (!hit) {
         l = l + lf;        // updateSetFree (:120-124)
         u = mf;
     } else {
-        if (f < h) {
+        if (m & 1u) {
             l = l + lf;    // bresenhamCellFree by an earlier beam
             l = l - lf;    // updateUnsetFree (:126-129)
         }
@@ -1069,9 +1074,76 @@ __device__ __forceinline__ int upd_off(int row, int tiles_x)
     return (row / TILE_H) * tiles_x * TILE_BLOCK_WORDS + (row % TILE_H) * TILE;
 }
 
-__device__ __forceinline__ bool quad_marked(const uint4 &h, const uint4 &f)
+constexpr int UPD_HIT_WORDS = UPD_TH * (TILE / 32);                  // one hit bit per tile cell
+constexpr int UPD_MARK_WORDS = (UPD_TILE_WORDS + UPD_HIT_WORDS + 3) & ~3;
+
+// ---- lane-balanced raster (S2D_RASTER_CHUNKED) ------------------------------------------------
+// A wave's beams cross a tile with very different free-step counts (none for most beams of a fan
+// far from the origin), so "one lane = one beam" leaves most lanes idle.  Instead each beam's walk
+// clipped to the tile becomes a SEGMENT record (64 per fan group, double-buffered) and is cut into
+// chunks of RC_K steps queued in a per-wave FIFO, drained 64 at a time, one chunk per lane: the lane
+// re-enters the Bresenham walk at the chunk's first step in closed form (one division) and walks
+// on incrementally.  The marks are order-free atomicMin, so any chunk order gives the same tile.
+#ifndef S2D_RASTER_CHUNKED
+#define S2D_RASTER_CHUNKED 0
+#endif
+#ifndef S2D_RC_K
+#define S2D_RC_K 8
+#endif
+constexpr int RC_K = S2D_RC_K;                                 // steps per chunk (power of two)
+constexpr int RC_MAX_STEPS = TILE > UPD_TH ? TILE : UPD_TH;     // free steps of one walk inside one tile
+constexpr int RC_MAX_CH = RC_MAX_STEPS / RC_K;                 // chunks per segment
+static_assert((RC_K & (RC_K - 1)) == 0 && RC_K >= 8 && RC_MAX_CH <= 8, "chunk entry: record (7 bits) | chunk << 7");
+constexpr int RC_RECS = 128;                                   // 2 fan groups x 64 lanes
+constexpr int RC_RING = 128;                                   // FIFO entries (u16): < 64 pending + one pass
+constexpr int RC_WAVE_WORDS = RC_RECS * 4 + RC_RING / 2;
+constexpr int UPD_CHUNK_WORDS = S2D_RASTER_CHUNKED ? (UPD_THREADS / 64) * RC_WAVE_WORDS : 0;
+constexpr int UPD_FIXED_WORDS = UPD_MARK_WORDS + UPD_CHUNK_WORDS;  // + rays + fan-group boxes (per scan size)
+static_assert(UPD_STRIDE >= TILE + 2 && UPD_TH >= 32, "per-lane dummy mark slots live in the row padding");
+
+__device__ __forceinline__ int lane_rank(unsigned long long m)  // set lanes below this one
 {
-    return ((h.x & f.x) & (h.y & f.y) & (h.z & f.z) & (h.w & f.w)) != W_NONE;
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+__device__ __forceinline__ void wave_lds_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Drain `cnt` (1..64) FIFO entries from position `head`: lane i walks entry head + i.
+__device__ __forceinline__ void rc_round(unsigned *__restrict__ marks, const uint4 *__restrict__ recs,
+                                         const unsigned short *__restrict__ ring, int head, int cnt, int lane,
+                                         int dummy)
+{
+    const unsigned e = ring[(head + lane) & (RC_RING - 1)];
+    const uint4 r = recs[e & (RC_RECS - 1)];
+    const int o = (int)(e >> 7) * RC_K;
+    const int li0 = (int)(r.x & 0xFFFFu);
+    const int das = (int)(signed char)(r.x >> 16);
+    const int dbs = (int)(signed char)(r.x >> 24);
+    const int err0 = (int)(r.y & 0xFFFFu);
+    const int da = (int)(r.z & 0xFFFFu);
+    const int db = (int)(r.z >> 16);
+    const unsigned ev = r.w;
+    int n = (int)(r.y >> 16) - o;
+    n = n < RC_K ? n : RC_K;
+    n = lane < cnt ? n : 0;
+    const unsigned num = (unsigned)err0 + (unsigned)o * (unsigned)db;
+    const int q = (int)udiv_small(num, (unsigned)(da > 0 ? da : 1));
+    // f = da - 1 - error_b: the walk steps the minor axis when f - db < 0 (error_b + db >= da)
+    int f = da - 1 - (int)(num - (unsigned)q * (unsigned)da);
+    int li = li0 + o * das + q * dbs;
+#pragma unroll
+    for (int j = 0; j < RC_K; ++j) {
+        atomicMin(&marks[j < n ? li : dummy], ev);  // bresenhamCellFree (:302-312)
+        const int g = f - db;
+        const int m = g >> 31;  // -1 on a minor step
+        f = g + (m & da);
+        li += das + (m & dbs);
+    }
 }
 
 // Grid: for level l, upd_parts[l] x count blocks (level-major, then part, then stream); part p of a
@@ -1081,10 +1153,17 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                  const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned smem[];
-    unsigned *first_hit = smem;                        // UPD_TILE_WORDS words
-    unsigned *first_free = smem + UPD_TILE_WORDS;      // UPD_TILE_WORDS words
-    unsigned *rays = smem + 2 * UPD_TILE_WORDS;        // max_points packed end cells
+    unsigned *marks = smem;                            // UPD_TILE_WORDS event words
+    unsigned *hitb = smem + UPD_TILE_WORDS;            // UPD_HIT_WORDS hit bits
+    unsigned *rays = smem + UPD_MARK_WORDS;            // max_points packed end cells
     int4 *gbox = reinterpret_cast<int4 *>(rays + ((max_points + 3) & ~3));  // per fan group: x0 y0 x1 y1
+    const int lane = threadIdx.x & 63;
+#if S2D_RASTER_CHUNKED
+    unsigned *rc_area = reinterpret_cast<unsigned *>(gbox + (max_points + 63) / 64) + (threadIdx.x >> 6) * RC_WAVE_WORDS;
+    uint4 *rc_recs = reinterpret_cast<uint4 *>(rc_area);
+    unsigned short *rc_ring = reinterpret_cast<unsigned short *>(rc_area + RC_RECS * 4);
+    const int rc_dummy = (lane & 31) * UPD_STRIDE + TILE + (lane >> 5);  // row padding, never applied
+#endif
     __shared__ int s_bbox[4];
 
     // level-major block order: every stream's level 0 (the largest) is dispatched first
@@ -1115,7 +1194,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     unsigned long long L = 0, R = 0;
     const float2 *pts = xy + (size_t)local * xy_stride;
     for (int b0 = tid & ~63; b0 < n; b0 += UPD_THREADS) {   // wave-uniform trip count
-        const int b = b0 + (tid & 63);
+        const int b = b0 + lane;
         unsigned r = RAY_INVALID;
         if (b < n) {
             r = make_ray(g, fr, pts[b]);
@@ -1137,7 +1216,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             gx1 = max(gx1, __shfl_xor(gx1, off, 64));
             gy1 = max(gy1, __shfl_xor(gy1, off, 64));
         }
-        if ((tid & 63) == 0) gbox[b0 >> 6] = make_int4(gx0, gy0, gx1, gy1);
+        if (lane == 0) gbox[b0 >> 6] = make_int4(gx0, gy0, gx1, gy1);
     }
     if (R) {
         atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
@@ -1148,7 +1227,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         L += __shfl_xor(L, off, 64);
         R += __shfl_xor(R, off, 64);
     }
-    if ((tid & 63) == 0 && R && part == 0) {
+    if (lane == 0 && R && part == 0) {
         atomicAdd(&state[s].step_cells, L);
         atomicAdd(&state[s].tot_cells, L);
         atomicAdd(&state[s].tot_rays, R);
@@ -1170,53 +1249,137 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         const int ty = ty0 + t / ntx, tx = tx0 + t % ntx;
         const int X0 = tx * TILE, Y0 = ty * UPD_TH;
         const int X1 = X0 + TILE, Y1 = Y0 + UPD_TH;
-        for (int k = tid; k < 2 * UPD_TILE_WORDS / 4; k += UPD_THREADS)
-            reinterpret_cast<uint4 *>(smem)[k] = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
+        for (int k = tid; k < UPD_MARK_WORDS / 4; k += UPD_THREADS)
+            reinterpret_cast<uint4 *>(smem)[k] = k < UPD_TILE_WORDS / 4 ? make_uint4(W_NONE, W_NONE, W_NONE, W_NONE)
+                                                                        : make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
         bool any = false;
+#if S2D_RASTER_CHUNKED
+        int rc_head = 0, rc_tail = 0, rc_par = 0, rc_guard0 = 0, rc_guard1 = 0;  // wave-uniform
+#endif
         for (int b0 = tid & ~63; b0 < n; b0 += UPD_THREADS) {
             // wave-uniform fan-group test (scalar)
             const int4 gb = gbox[b0 >> 6];
             const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
             const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
             if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
-            const int b = b0 + (tid & 63);
-            if (b >= n) continue;
-            const unsigned r = rays[b];
-            if (r == RAY_INVALID) continue;
-            const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-            if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
-            if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {
-                atomicMin(&first_hit[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], (unsigned)b);  // bresenhamCellOcc (:266)
-                any = true;
+            const int b = b0 + lane;
+            const unsigned r = b < n ? rays[b] : RAY_INVALID;
+            int scnt = 0;           // free steps of this beam inside the tile
+            RayWalk w = {};
+            int lo_i = 0, q = 0, err = 0;
+            if (r != RAY_INVALID) {
+                const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+                if (!(max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1)) {
+                    if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {  // bresenhamCellOcc (:266)
+                        const int c = (y1 - Y0) * TILE + (x1 - X0);
+                        atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
+                        atomicOr(&hitb[c >> 5], 1u << (c & 31));
+                        any = true;
+                    }
+                    w = ray_walk(x0, y0, x1, y1);
+                    int hi_i;
+                    const bool in = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i)
+                                              : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
+                    if (in) {
+                        if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
+                        if (lo_i <= hi_i) {
+                            scnt = hi_i - lo_i + 1;
+                            const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
+                            q = (int)udiv_small(num, (unsigned)w.da);
+                            err = (int)(num - (unsigned)q * (unsigned)w.da);
+                            any = true;
+                        }
+                    }
+                }
             }
-            RayWalk w = ray_walk(x0, y0, x1, y1);
-            int lo_i, hi_i;
-            bool in = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i) : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
-            if (!in) continue;
-            if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
-            if (lo_i > hi_i) continue;
-            any = true;
-            const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
-            const int q = (int)udiv_small(num, (unsigned)w.da);
-            int err = (int)(num - (unsigned)q * (unsigned)w.da);
-            // local LDS index of step lo_i and its increments along the major / minor axis
+            const unsigned ev = 2u * (unsigned)b + 1u;
+            // LDS index of step lo_i and its increments along the major / minor axis
             const int la = w.x_major ? 1 : UPD_STRIDE;
             const int lb = w.x_major ? UPD_STRIDE : 1;
             const int ax = w.a0 + w.sa * lo_i - (w.x_major ? X0 : Y0);
             const int bx = w.b0 + w.sb * q - (w.x_major ? Y0 : X0);
-            int li = ax * la + bx * lb;
+            const int li = ax * la + bx * lb;
             const int da_step = w.sa * la, db_step = w.sb * lb;
-            for (int i = lo_i; i <= hi_i; ++i) {
-                atomicMin(&first_free[li], (unsigned)b);  // bresenhamCellFree (:302-312)
-                li += da_step;
-                err += w.db;
-                if (err >= w.da) {
-                    err -= w.da;
-                    li += db_step;
+#if S2D_RASTER_CHUNKED
+            const unsigned long long segm = __ballot(scnt > 0);
+            if (segm == 0) continue;
+            // records of this parity are reused: drain every queued chunk of the group that used them
+            const int guard = rc_par ? rc_guard1 : rc_guard0;
+            while (rc_head < guard) {
+                const int c = min(64, rc_tail - rc_head);
+                rc_round(marks, rc_recs, rc_ring, rc_head, c, lane, rc_dummy);
+                rc_head += c;
+            }
+            const int slot = rc_par * 64 + lane;
+            if (scnt > 0)
+                rc_recs[slot] = make_uint4((unsigned)li | ((unsigned)da_step & 0xFFu) << 16 | ((unsigned)db_step & 0xFFu) << 24,
+                                           (unsigned)err | (unsigned)scnt << 16, (unsigned)w.da | (unsigned)w.db << 16, ev);
+            const int nch = (scnt + RC_K - 1) / RC_K;
+            for (int c = 0;; ++c) {  // pass c queues chunk c of every segment that has one
+                const unsigned long long m = __ballot(nch > c);
+                if (m == 0) break;
+                if (nch > c) rc_ring[(rc_tail + lane_rank(m)) & (RC_RING - 1)] = (unsigned short)(slot | (c << 7));
+                rc_tail += __popcll(m);
+                wave_lds_fence();
+                if (rc_tail - rc_head >= 64) {
+                    rc_round(marks, rc_recs, rc_ring, rc_head, 64, lane, rc_dummy);
+                    rc_head += 64;
                 }
             }
+            if (rc_par) rc_guard1 = rc_tail; else rc_guard0 = rc_tail;
+            rc_par ^= 1;
+#else
+#ifdef S2D_VISITS
+            {
+                const unsigned long long am = __ballot(scnt > 0);
+                int mx = scnt, sm = scnt;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    mx = max(mx, __shfl_xor(mx, off, 64));
+                    sm += __shfl_xor(sm, off, 64);
+                }
+                if (lane == 0) {
+                    atomicAdd(&g_stamps[4], 1ull);
+                    atomicAdd(&g_stamps[5], (unsigned long long)__popcll(am));
+                    atomicAdd(&g_stamps[6], (unsigned long long)sm);
+                    atomicAdd(&g_stamps[7], (unsigned long long)mx);
+                }
+            }
+#endif
+#ifdef S2D_DIAG_NOSTEP
+            continue;  // diagnostic build only: group setup cost without the walk
+#endif
+            if (scnt <= 0) continue;
+            // incremental walk, f = da - 1 - error_b: the minor axis steps when f - db < 0; byte
+            // offsets into the mark array, two steps per trip
+            const int dab = da_step * 4, dbb = db_step * 4;
+            const int da_ = w.da, db_ = w.db;
+            int f = da_ - 1 - err;
+            char *pm = reinterpret_cast<char *>(marks) + li * 4;
+            int i = 0;
+            for (; i + 1 < scnt; i += 2) {
+                atomicMin(reinterpret_cast<unsigned *>(pm), ev);  // bresenhamCellFree (:302-312)
+                int g2 = f - db_;
+                int m = g2 >> 31;
+                f = g2 + (m & da_);
+                pm += dab + (m & dbb);
+                atomicMin(reinterpret_cast<unsigned *>(pm), ev);
+                g2 = f - db_;
+                m = g2 >> 31;
+                f = g2 + (m & da_);
+                pm += dab + (m & dbb);
+            }
+            if (i < scnt) atomicMin(reinterpret_cast<unsigned *>(pm), ev);
+#endif
         }
+#if S2D_RASTER_CHUNKED
+        while (rc_head < rc_tail) {
+            const int c = min(64, rc_tail - rc_head);
+            rc_round(marks, rc_recs, rc_ring, rc_head, c, lane, rc_dummy);
+            rc_head += c;
+        }
+#endif
         const bool tile_any = __syncthreads_or(any);
 #ifdef S2D_STAMPS
         S2D_STAMP(t_c);
@@ -1224,24 +1387,25 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         t_b = t_c;
 #endif
         if (!tile_any) continue;
-        // apply: thread owns quads q = tid + j * 256 (16 quads per 64-cell row): 16-B LDS reads,
-        // 16-B global loads / stores of both planes for every quad holding a mark.  Cells outside
-        // the map (padding of edge tiles) never carry marks and are rewritten unchanged.
+        // apply: thread owns quads q = tid + j * 256 (16 quads per 64-cell row): 16-B LDS reads of the
+        // event words, 16-B global loads / stores of both planes for every quad holding a mark.  Cells
+        // outside the map (padding of edge tiles) never carry marks and are rewritten unchanged.
         // quad qi: LDS row qi / 16, storage tile (tx, (Y0 + row) / TILE_H), storage row (Y0 + row) % TILE_H
         float *tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
         int *tu = reinterpret_cast<int *>(tl + TILE_CELLS);
-        uint4 qh[UPD_QUADS], qf[UPD_QUADS];
+        uint4 qm[UPD_QUADS];
+        unsigned qh[UPD_QUADS];
         float4 ql[UPD_QUADS];
         int4 qu[UPD_QUADS];
-        bool qm[UPD_QUADS];
+        bool qa[UPD_QUADS];
 #pragma unroll
         for (int j = 0; j < UPD_QUADS; ++j) {
             const int qi = tid + j * UPD_THREADS;
             const int row = qi >> 4, c4 = (qi & 15) << 2;
-            qh[j] = *reinterpret_cast<const uint4 *>(&first_hit[row * UPD_STRIDE + c4]);
-            qf[j] = *reinterpret_cast<const uint4 *>(&first_free[row * UPD_STRIDE + c4]);
-            qm[j] = quad_marked(qh[j], qf[j]);
-            if (qm[j]) {
+            qm[j] = *reinterpret_cast<const uint4 *>(&marks[row * UPD_STRIDE + c4]);
+            qh[j] = hitb[row * (TILE / 32) + (c4 >> 5)] >> (c4 & 31);
+            qa[j] = (qm[j].x & qm[j].y & qm[j].z & qm[j].w) != W_NONE;
+            if (qa[j]) {
                 ql[j] = *reinterpret_cast<const float4 *>(&tl[upd_off(row, g.tiles_x) + c4]);
 #if S2D_APPLY_UPD_LOAD
                 qu[j] = *reinterpret_cast<const int4 *>(&tu[upd_off(row, g.tiles_x) + c4]);
@@ -1250,22 +1414,22 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         }
 #pragma unroll
         for (int j = 0; j < UPD_QUADS; ++j) {
-            if (!qm[j]) continue;
+            if (!qa[j]) continue;
             const int qi = tid + j * UPD_THREADS;
             const int row = qi >> 4, c4 = (qi & 15) << 2;
 #if S2D_APPLY_UPD_LOAD
-            touched += apply_cell(ql[j].x, qu[j].x, qh[j].x, qf[j].x, lf, lo, mark_free, mark_occ);
-            touched += apply_cell(ql[j].y, qu[j].y, qh[j].y, qf[j].y, lf, lo, mark_free, mark_occ);
-            touched += apply_cell(ql[j].z, qu[j].z, qh[j].z, qf[j].z, lf, lo, mark_free, mark_occ);
-            touched += apply_cell(ql[j].w, qu[j].w, qh[j].w, qf[j].w, lf, lo, mark_free, mark_occ);
+            touched += apply_cell(ql[j].x, qu[j].x, qm[j].x, qh[j] & 1u, lf, lo, mark_free, mark_occ);
+            touched += apply_cell(ql[j].y, qu[j].y, qm[j].y, qh[j] & 2u, lf, lo, mark_free, mark_occ);
+            touched += apply_cell(ql[j].z, qu[j].z, qm[j].z, qh[j] & 4u, lf, lo, mark_free, mark_occ);
+            touched += apply_cell(ql[j].w, qu[j].w, qm[j].w, qh[j] & 8u, lf, lo, mark_free, mark_occ);
             *reinterpret_cast<float4 *>(&tl[upd_off(row, g.tiles_x) + c4]) = ql[j];
             *reinterpret_cast<int4 *>(&tu[upd_off(row, g.tiles_x) + c4]) = qu[j];
 #else
             int u[4];
-            const int t0 = apply_cell(ql[j].x, u[0], qh[j].x, qf[j].x, lf, lo, mark_free, mark_occ);
-            const int t1 = apply_cell(ql[j].y, u[1], qh[j].y, qf[j].y, lf, lo, mark_free, mark_occ);
-            const int t2 = apply_cell(ql[j].z, u[2], qh[j].z, qf[j].z, lf, lo, mark_free, mark_occ);
-            const int t3 = apply_cell(ql[j].w, u[3], qh[j].w, qf[j].w, lf, lo, mark_free, mark_occ);
+            const int t0 = apply_cell(ql[j].x, u[0], qm[j].x, qh[j] & 1u, lf, lo, mark_free, mark_occ);
+            const int t1 = apply_cell(ql[j].y, u[1], qm[j].y, qh[j] & 2u, lf, lo, mark_free, mark_occ);
+            const int t2 = apply_cell(ql[j].z, u[2], qm[j].z, qh[j] & 4u, lf, lo, mark_free, mark_occ);
+            const int t3 = apply_cell(ql[j].w, u[3], qm[j].w, qh[j] & 8u, lf, lo, mark_free, mark_occ);
             touched += t0 + t1 + t2 + t3;
             const int o = upd_off(row, g.tiles_x) + c4;
             *reinterpret_cast<float4 *>(&tl[o]) = ql[j];
@@ -1285,8 +1449,11 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);
-    if ((tid & 63) == 0 && touched) atomicAdd(&state[s].tot_touched, (unsigned long long)touched);
+    if (lane == 0 && touched) atomicAdd(&state[s].tot_touched, (unsigned long long)touched);
 #ifdef S2D_STAMPS
+#ifdef S2D_STAMPS_LVL
+    if (lvl != S2D_STAMPS_LVL) return;
+#endif
     if (tid == 0) {
         atomicAdd(&g_stamps[0], c_setup);
         atomicAdd(&g_stamps[1], c_raster);
@@ -1295,7 +1462,6 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     }
 #endif
 }
-
 
 // --------------------------------------------------------------------------- utility kernels
 __global__ void hs_fill_cells_kernel(float *__restrict__ words, size_t n)

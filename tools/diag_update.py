@@ -22,7 +22,10 @@ torch.cuda.synchronize()
 q = f.queue_stats(); kt = f.kernel_times()
 print("kernel ms:", kt)
 tot = q["cyc_setup"] + q["cyc_raster"] + q["cyc_apply"]
-blocks = B * 3
+blocks = B * (1 if os.environ.get("LVL_ONLY") else 3)
 print("per block: setup %.0f raster %.0f apply %.0f cycles; nonempty tiles/block %.1f" % (
     q["cyc_setup"] / blocks, q["cyc_raster"] / blocks, q["cyc_apply"] / blocks, q["tiles"] / blocks))
 print("shares: setup %.3f raster %.3f apply %.3f" % (q["cyc_setup"] / tot, q["cyc_raster"] / tot, q["cyc_apply"] / tot))
+if os.environ.get("VISITS"):
+    print("group visits %d, active lanes/visit %.1f, steps/visit %.1f, max steps/visit %.1f, lane util %.3f" % (
+        q["items"], q["segments"] / q["items"], q["whole"] / q["items"], q["overflow"] / q["items"], q["whole"] / (64.0 * q["overflow"])))

@@ -533,6 +533,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--no-copy-probe", action="store_true", help="skip the copy-bandwidth probe")
+    ap.add_argument("--input", choices=["ranges", "points"], default="ranges",
+                    help="hector: raw LaserScan ranges through the on-device ingest (scanCallback, default) or "
+                         "pre-converted DataContainer points")
     args = ap.parse_args()
 
     import torch
@@ -565,10 +568,15 @@ def main():
     # ---- synthetic input, resident in HBM before timing: [step][stream][1081][2] ----
     t0 = time.perf_counter()
     S = synth.make_streams(B, T, seed=12345 + rank * B)
-    pts = np.ascontiguousarray(S.points.transpose(1, 0, 2, 3))
-    cnt = np.ascontiguousarray(S.counts.T.astype(np.int32))
-    d_pts = torch.from_numpy(pts).to(dev)
-    d_cnt = torch.from_numpy(cnt).to(dev)
+    from_ranges = args.input == "ranges"
+    if from_ranges:  # LaserScan ranges [step][stream][1081] float32
+        rng_in = np.ascontiguousarray(S.ranges.transpose(1, 0, 2))
+        d_rng = torch.from_numpy(rng_in).to(dev)
+    else:
+        pts = np.ascontiguousarray(S.points.transpose(1, 0, 2, 3))
+        cnt = np.ascontiguousarray(S.counts.T.astype(np.int32))
+        d_pts = torch.from_numpy(pts).to(dev)
+        d_cnt = torch.from_numpy(cnt).to(dev)
     log(f"[bench] rank {rank}: generated {B} streams x {T} scans in {time.perf_counter() - t0:.1f}s")
 
     fleet = HectorFleet(B, 0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], max_points=1081)
@@ -578,11 +586,23 @@ def main():
     n_log = min(2, B)
     d_plog = torch.zeros((T, n_log, 3), dtype=torch.float32, device=dev)
     fleet.set_pose_log(d_plog.data_ptr(), n_log, T)
-    stride = pts.shape[2]
-    step_bytes = pts.shape[1] * pts.shape[2] * 8
+    if from_ranges:
+        # the node's filters with the generator's own beam directions as the unit-vector cache, so the
+        # device DataContainers equal synth's points (the pose check below replays those)
+        from slam2d.hector import HsLaser
+        nb = S.ranges.shape[2]
+        ang = synth.beam_angles(nb)
+        fleet.set_laser(HsLaser.defaults(nb, float(ang[0]), float(ang[1] - ang[0])),
+                        unit_vectors=np.stack([np.cos(ang), np.sin(ang)], 1))
 
-    def step(t):
-        fleet.step_device(d_pts.data_ptr() + t * step_bytes, stride, d_cnt[t].data_ptr(), hip_stream=hs)
+        def step(t):
+            fleet.step_ranges_device(d_rng[t].data_ptr(), nb, hip_stream=hs)
+    else:
+        stride = pts.shape[2]
+        step_bytes = pts.shape[1] * pts.shape[2] * 8
+
+        def step(t):
+            fleet.step_device(d_pts.data_ptr() + t * step_bytes, stride, d_cnt[t].data_ptr(), hip_stream=hs)
 
     for t in range(W):
         step(t)
@@ -647,6 +667,8 @@ def main():
                                       f"{cfg['levels']} levels, 1081-beam scans, map update every scan",
                           "config": args.config, "streams_per_gpu": B, "global_batch": B * world,
                           "map_size": cfg["map_size"], "levels": cfg["levels"], "beams": 1081,
+                          "input": ("LaserScan ranges (on-device ingest in the timed region)" if from_ranges
+                                    else "DataContainer points"),
                           "parallelism": f"replicas x{world}"},
                "roofline": roof, "cpu_baseline": cpu, "pose_vs_ref": pose}
         if cpu:

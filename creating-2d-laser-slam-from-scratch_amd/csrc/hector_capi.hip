@@ -82,6 +82,14 @@ struct hs_ctx {
     int update_single = 1;  // hs_update_kernel (per stream-level, default) or bin + tile kernels
     hipStream_t pstream[MAX_PARTS] = {};
     hipEvent_t ev_start = nullptr, ev_done[MAX_PARTS] = {};
+    // scan ingest (hs_set_laser): unit vectors, geometry, the batch's DataContainers
+    bool has_laser = false;
+    IngestGeom ingest{};
+    double2 *d_cs = nullptr;
+    float2 *d_ixy = nullptr;
+    int *d_in = nullptr;
+    float2 *d_iorigo = nullptr;
+    float *d_ranges1 = nullptr;
 };
 
 namespace {
@@ -411,6 +419,11 @@ int hs_destroy(hs_ctx *c)
     hipFree(c->d_items);
     hipFree(c->d_wholes);
     hipFree(c->d_wq);
+    hipFree(c->d_cs);
+    hipFree(c->d_ixy);
+    hipFree(c->d_in);
+    hipFree(c->d_iorigo);
+    hipFree(c->d_ranges1);
     for (auto &p : c->ev_used) {
         hipEventDestroy(p.a);
         hipEventDestroy(p.b);
@@ -602,6 +615,116 @@ int hs_step_batch_device(hs_ctx *c, int stream_begin, int count, const float *d_
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
     return launch_step(c, stream_begin, count, (const float2 *)d_xy, xy_stride, d_n, (const float2 *)d_origo, d_hints,
                        MODE_PROCESS, nullptr, nullptr, s);
+}
+
+void hs_default_laser(hs_laser *L, int n_beams, float angle_min, float angle_increment)
+{
+    if (!L) return;
+    memset(L, 0, sizeof(*L));
+    L->n_beams = n_beams;
+    L->angle_min = angle_min;
+    L->angle_increment = angle_increment;
+    L->range_min = 0.0f;
+    L->range_cutoff = 30.0;                              // projectLaser(..., 30.0)  hector_slam.cc:193
+    L->basis[0] = L->basis[4] = L->basis[8] = 1.0;
+    L->sqr_laser_min_dist = (float)(0.2 * 0.2);          // hector_slam.cc:151-152
+    L->sqr_laser_max_dist = (float)(30.0 * 30.0);        // :154-155
+    L->use_max_scan_range = 20.0;                        // :129
+    L->laser_z_min_value = -1.0f;                        // :157-158
+    L->laser_z_max_value = 1.0f;                         // :160-161
+}
+
+int hs_set_laser(hs_ctx *c, const hs_laser *L, const double *unit_vectors)
+{
+    if (!c || !L) return fail(HS_EINVAL, "NULL argument");
+    if (L->n_beams < 0 || L->n_beams > c->max_points) return fail(HS_EINVAL, "n_beams must be in [0, max_points]");
+    IngestGeom &g = c->ingest;
+    g.n = L->n_beams;
+    g.cutoff = L->range_cutoff;
+    g.range_min = L->range_min;
+    memcpy(g.tf, L->basis, sizeof(double) * 9);
+    memcpy(g.tf + 9, L->origin, sizeof(double) * 3);
+    g.sqr_min = L->sqr_laser_min_dist;
+    g.sqr_max = L->sqr_laser_max_dist;
+    g.use_max_sq = L->use_max_scan_range * L->use_max_scan_range;  // double product, hector_slam.cc:344
+    g.z_min = L->laser_z_min_value;
+    g.z_max = L->laser_z_max_value;
+    g.scale = c->geom.lv[0].scale;                                 // getScaleToMap (level 0)
+    g.origo = make_float2((float)L->origin[0] * g.scale, (float)L->origin[1] * g.scale);  // :329
+    std::vector<double> cs((size_t)2 * (L->n_beams > 0 ? L->n_beams : 1));
+    for (int i = 0; i < L->n_beams; ++i) {
+        if (unit_vectors) {
+            cs[2 * i] = unit_vectors[2 * i];
+            cs[2 * i + 1] = unit_vectors[2 * i + 1];
+        } else {  // laser_geometry getUnitVectors_: cos / sin(angle_min + (double)i * angle_increment)
+            const double a = (double)L->angle_min + (double)i * (double)L->angle_increment;
+            cs[2 * i] = cos(a);
+            cs[2 * i + 1] = sin(a);
+        }
+    }
+    hipError_t e;
+    if (!c->d_cs) {
+        if ((e = hipMalloc(&c->d_cs, sizeof(double2) * (size_t)c->max_points)) != hipSuccess ||
+            (e = hipMalloc(&c->d_ixy, sizeof(float2) * (size_t)c->B * c->max_points)) != hipSuccess ||
+            (e = hipMalloc(&c->d_in, sizeof(int) * (size_t)c->B)) != hipSuccess ||
+            (e = hipMalloc(&c->d_iorigo, sizeof(float2) * (size_t)c->B)) != hipSuccess ||
+            (e = hipMalloc(&c->d_ranges1, sizeof(float) * (size_t)c->max_points)) != hipSuccess)
+            return fail(HS_ENOMEM, "hipMalloc(ingest)", e);
+    }
+    if (L->n_beams > 0)
+        HCHK(hipMemcpyAsync(c->d_cs, cs.data(), sizeof(double2) * L->n_beams, hipMemcpyHostToDevice, c->stream));
+    HCHK(hipStreamSynchronize(c->stream));
+    c->has_laser = true;
+    return HS_OK;
+}
+
+int hs_ingest_batch_device(hs_ctx *c, int count, const float *d_ranges, int range_stride, float *d_xy, int xy_stride,
+                           int *d_n, float *d_origo, void *hip_stream)
+{
+    if (!c || count < 0 || (count > 0 && (!d_ranges || !d_xy || !d_n))) return fail(HS_EINVAL, "bad ingest arguments");
+    if (!c->has_laser) return fail(HS_EINVAL, "hs_set_laser not called");
+    if (range_stride < c->ingest.n || xy_stride < c->ingest.n) return fail(HS_EINVAL, "stride < n_beams");
+    if (count == 0) return HS_OK;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipLaunchKernelGGL(hs_ingest_kernel, dim3(count), dim3(256), 0, s, c->ingest, c->d_cs, d_ranges, range_stride,
+                       (float2 *)d_xy, xy_stride, d_n, (float2 *)d_origo);
+    HCHK(hipGetLastError());
+    return HS_OK;
+}
+
+int hs_step_ranges_batch_device(hs_ctx *c, int stream_begin, int count, const float *d_ranges, int range_stride,
+                                const float *d_hints, void *hip_stream)
+{
+    if (!c || stream_begin < 0 || count < 0 || stream_begin + count > c->B) return fail(HS_EINVAL, "bad batch arguments");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    int rc = hs_ingest_batch_device(c, count, d_ranges, range_stride, (float *)c->d_ixy, c->max_points, c->d_in,
+                                    (float *)c->d_iorigo, s);
+    if (rc != HS_OK || count == 0) return rc;
+    return launch_step(c, stream_begin, count, c->d_ixy, c->max_points, c->d_in, c->d_iorigo, d_hints, MODE_PROCESS,
+                       nullptr, nullptr, s);
+}
+
+int hs_update_ranges(hs_ctx *c, int stream, const float *ranges, float pose_out[3], float cov_out[9], int *did_update_out)
+{
+    if (check_stream(c, stream) != HS_OK) return fail(HS_EINVAL, "bad ctx/stream");
+    if (!c->has_laser) return fail(HS_EINVAL, "hs_set_laser not called");
+    if (c->ingest.n > 0 && !ranges) return fail(HS_EINVAL, "ranges is NULL");
+    if (c->ingest.n > 0)
+        HCHK(hipMemcpyAsync(c->d_ranges1, ranges, sizeof(float) * c->ingest.n, hipMemcpyHostToDevice, c->stream));
+    int rc = hs_ingest_batch_device(c, 1, c->d_ranges1, c->max_points, (float *)c->d_pts1, c->max_points, c->d_n1,
+                                    (float *)c->d_origo1, c->stream);
+    if (rc != HS_OK) return rc;
+    // scanCallback: startEstimate = getLastScanMatchPose() (hector_slam.cc:201), i.e. no explicit hint
+    rc = launch_step(c, stream, 1, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, nullptr, MODE_PROCESS, c->d_out_pose,
+                     c->d_out_cov, c->stream);
+    if (rc != HS_OK) return rc;
+    StreamState st;
+    HCHK(hipMemcpyAsync(&st, c->d_state + stream, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+    HCHK(hipStreamSynchronize(c->stream));
+    if (pose_out) memcpy(pose_out, st.pose, sizeof(float) * 3);
+    if (cov_out) memcpy(cov_out, st.cov, sizeof(float) * 9);
+    if (did_update_out) *did_update_out = st.do_update;
+    return HS_OK;
 }
 
 int hs_get_poses(hs_ctx *c, float *poses_out, float *covs_out, int *did_update_out, int64_t *cells_out)

@@ -1489,4 +1489,71 @@ __global__ void hs_publish_kernel(const float *__restrict__ lvw, LevelGeom g, in
     }
 }
 
+// ---- scan ingest ---------------------------------------------------------------------------------
+// HectorMappingRos::scanCallback (hector_slam.cc:186-198) for a batch of range arrays, one 256-thread
+// workgroup per stream: laser_geometry's projectLaser(scan, cloud, 30.0) (double products of the
+// cached unit vectors, rounded to the float Point32) and rosPointCloudToDataContainer (:320-362)
+// statement by statement, then an order-preserving compaction (wave ballots + a per-chunk prefix over
+// the 4 waves), so point k of the DataContainer is the k-th surviving beam as in the node's loop.
+struct IngestGeom {
+    double cutoff, use_max_sq;
+    double tf[12];  // basis rows, origin
+    float range_min, sqr_min, sqr_max, z_min, z_max, scale;
+    float2 origo;
+    int n;
+};
+
+__global__ void __launch_bounds__(256)
+hs_ingest_kernel(IngestGeom ig, const double2 *__restrict__ cs, const float *__restrict__ ranges, int rstride,
+                 float2 *__restrict__ xy, int xy_stride, int *__restrict__ n_out, float2 *__restrict__ origo_out)
+{
+    __shared__ int s_w[4];
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const float *r = ranges + (size_t)s * rstride;
+    float2 *out = xy + (size_t)s * xy_stride;
+    int base = 0;
+    for (int b0 = 0; b0 < ig.n; b0 += 256) {
+        const int i = b0 + tid;
+        bool keep = false;
+        float2 p = make_float2(0.0f, 0.0f);
+        if (i < ig.n) {
+            const float range = r[i];
+            if (((double)range < ig.cutoff) && (range >= ig.range_min)) {  // projectLaser_
+                const double2 u = cs[i];
+                const float x = (float)((double)range * u.x);
+                const float y = (float)((double)range * u.y);
+                const float z = 0.0f;
+                const float d2 = __fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y));          // :334
+                keep = (d2 > ig.sqr_min) && (d2 < ig.sqr_max);                          // :336
+                if ((x < 0.0f) && (d2 < 0.50f)) keep = false;                           // :338-341
+                if ((double)d2 > ig.use_max_sq) keep = false;                           // :344-345
+                if (keep) {
+                    const double vx = (double)x, vy = (double)y, vz = (double)z;        // :348 tf dot products
+                    const double px = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(ig.tf[0], vx), __dmul_rn(ig.tf[1], vy)),
+                                                          __dmul_rn(ig.tf[2], vz)), ig.tf[9]);
+                    const double py = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(ig.tf[3], vx), __dmul_rn(ig.tf[4], vy)),
+                                                          __dmul_rn(ig.tf[5], vz)), ig.tf[10]);
+                    const double pz = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(ig.tf[6], vx), __dmul_rn(ig.tf[7], vy)),
+                                                          __dmul_rn(ig.tf[8], vz)), ig.tf[11]);
+                    const float zl = (float)(pz - ig.tf[11]);                            // :351
+                    keep = zl > ig.z_min && zl < ig.z_max;                               // :353
+                    p = make_float2(__fmul_rn((float)px, ig.scale), __fmul_rn((float)py, ig.scale));  // :356
+                }
+            }
+        }
+        const unsigned long long m = __ballot(keep);
+        if (lane == 0) s_w[wv] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int k = 0; k < wv; ++k) off += s_w[k];
+        if (keep) out[off + lane_rank(m)] = p;
+        base += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        n_out[s] = base;
+        if (origo_out) origo_out[s] = ig.origo;
+    }
+}
+
 }  // namespace s2d

@@ -59,6 +59,12 @@ def _declare(L):
     L.hs_get_stream.argtypes = [_p]
     L.hs_set_timing.argtypes = [_p, _i]
     L.hs_get_kernel_times.argtypes = [_p, _p, _p, _i]
+    L.hs_default_laser.restype = None
+    L.hs_default_laser.argtypes = [_p, _i, _f, _f]
+    L.hs_set_laser.argtypes = [_p, _p, _p]
+    L.hs_ingest_batch_device.argtypes = [_p, _i, _p, _i, _p, _i, _p, _p, _p]
+    L.hs_step_ranges_batch_device.argtypes = [_p, _i, _i, _p, _i, _p, _p]
+    L.hs_update_ranges.argtypes = [_p, _i, _p, _p, _p, P(_i)]
     # GMapping particle path (include/slam2d/gmapping.h)
     D = C.c_double
     L.gm_version.restype = C.c_char_p

@@ -78,6 +78,28 @@ class DataContainer:
         return d
 
 
+class HsLaser(C.Structure):
+    """include/slam2d/hector.h hs_laser (the node's scan geometry and filter parameters)."""
+    _fields_ = [("n_beams", C.c_int), ("angle_min", C.c_float), ("angle_increment", C.c_float),
+                ("range_min", C.c_float), ("range_cutoff", C.c_double), ("basis", C.c_double * 9),
+                ("origin", C.c_double * 3), ("sqr_laser_min_dist", C.c_float), ("sqr_laser_max_dist", C.c_float),
+                ("use_max_scan_range", C.c_double), ("laser_z_min_value", C.c_float),
+                ("laser_z_max_value", C.c_float)]
+
+    @classmethod
+    def defaults(cls, n_beams: int, angle_min: float, angle_increment: float) -> "HsLaser":
+        L = cls()
+        _lib.lib().hs_default_laser(C.byref(L), n_beams, angle_min, angle_increment)
+        return L
+
+    def as_oracle_dict(self) -> dict:
+        """The same parameters in the form oracle.ingest takes (tests only)."""
+        return {"range_cutoff": self.range_cutoff, "range_min": self.range_min,
+                "tf": list(self.basis) + list(self.origin), "sqr_min": self.sqr_laser_min_dist,
+                "sqr_max": self.sqr_laser_max_dist, "use_max": self.use_max_scan_range,
+                "z_min": self.laser_z_min_value, "z_max": self.laser_z_max_value}
+
+
 class HectorFleet:
     """B independent Hector SLAM streams resident in HBM (one MapRepMultiMap pyramid each)."""
 
@@ -189,6 +211,38 @@ class HectorFleet:
         check(self.L.hs_step_batch_device(self.h, stream_begin, count, C.c_void_p(d_xy), int(xy_stride),
                                           C.c_void_p(d_n), C.c_void_p(d_origo or None), C.c_void_p(d_hints or None),
                                           C.c_void_p(hip_stream or None)), "hs_step_batch_device")
+
+    # ---- scan ingest (LaserScan -> DataContainer on the device), hector_slam.cc:186-198, 320-362 ----
+    def set_laser(self, laser: "HsLaser", unit_vectors=None):
+        """HectorMappingRos's scan geometry + filters (hs_set_laser); unit_vectors [n, 2] double or None
+        (computed with the host libm as laser_geometry's getUnitVectors_)."""
+        uv = None
+        if unit_vectors is not None:
+            uv = np.ascontiguousarray(unit_vectors, np.float64).reshape(-1)
+        check(self.L.hs_set_laser(self.h, C.byref(laser), _fp(uv) if uv is not None else None), "hs_set_laser")
+
+    def ingest_device(self, count: int, d_ranges: int, range_stride: int, d_xy: int, xy_stride: int, d_n: int,
+                      d_origo: int = 0, hip_stream: int = 0):
+        check(self.L.hs_ingest_batch_device(self.h, count, C.c_void_p(d_ranges), int(range_stride), C.c_void_p(d_xy),
+                                            int(xy_stride), C.c_void_p(d_n), C.c_void_p(d_origo or None),
+                                            C.c_void_p(hip_stream or None)), "hs_ingest_batch_device")
+
+    def step_ranges_device(self, d_ranges: int, range_stride: int, d_hints: int = 0, stream_begin: int = 0,
+                           count: int | None = None, hip_stream: int = 0):
+        """scanCallback for every stream: ingest + HectorSlamProcessor::update (device pointers)."""
+        count = self.B - stream_begin if count is None else count
+        check(self.L.hs_step_ranges_batch_device(self.h, stream_begin, count, C.c_void_p(d_ranges), int(range_stride),
+                                                 C.c_void_p(d_hints or None), C.c_void_p(hip_stream or None)),
+              "hs_step_ranges_batch_device")
+
+    def update_ranges(self, stream: int, ranges):
+        """scanCallback for one stream from host ranges (float32 [n_beams])."""
+        r = np.ascontiguousarray(ranges, np.float32)
+        pose = np.zeros(3, np.float32)
+        cov = np.zeros(9, np.float32)
+        did = C.c_int()
+        check(self.L.hs_update_ranges(self.h, stream, _fp(r), _fp(pose), _fp(cov), C.byref(did)), "hs_update_ranges")
+        return pose, cov.reshape(3, 3), bool(did.value)
 
     def poses(self):
         p = np.zeros((self.B, 3), np.float32)

@@ -98,6 +98,43 @@ int hs_set_map(hs_ctx *ctx, int stream, int level, const float *logodds, const i
  * Results stay on device; read them with hs_get_poses (synchronising) when needed. */
 int hs_step_batch_device(hs_ctx *ctx, int stream_begin, int count, const float *d_xy, int xy_stride, const int *d_n,
                          const float *d_origo, const float *d_hints, void *hip_stream);
+/* ---- scan ingest (LaserScan -> DataContainer), on the device ------------------------------------
+ * HectorMappingRos::scanCallback (lesson4/src/hector_mapping/hector_slam.cc:186-198): laser_geometry's
+ * projectLaser(scan, cloud, 30.0) then rosPointCloudToDataContainer (:320-362), restated for a batch of
+ * raw range arrays.  Field names follow the node's parameters (hector_slam.cc:129, 151-161). */
+typedef struct hs_laser {
+    int n_beams;                 /* ranges per scan (<= max_points of the context) */
+    float angle_min;             /* sensor_msgs/LaserScan angle_min, angle_increment (float32 fields) */
+    float angle_increment;
+    float range_min;             /* LaserScan range_min: projectLaser keeps range >= range_min */
+    double range_cutoff;         /* projectLaser's range_cutoff (30.0 at hector_slam.cc:193): keeps range < it */
+    double basis[9];             /* laserTransform_ (base frame <- scan frame) rotation, tf::Matrix3x3 rows */
+    double origin[3];            /* laserTransform_ translation (laserPos) */
+    float sqr_laser_min_dist;    /* p_sqr_laser_min_dist_ = (float)(laser_min_dist^2)       (:151-152) */
+    float sqr_laser_max_dist;    /* p_sqr_laser_max_dist_ = (float)(laser_max_dist^2)       (:154-155) */
+    double use_max_scan_range;   /* p_use_max_scan_range_                                    (:129) */
+    float laser_z_min_value;     /* p_laser_z_min_value_ / p_laser_z_max_value_              (:157-161) */
+    float laser_z_max_value;
+} hs_laser;
+/* The node's defaults for an n-beam scan (laser_min_dist 0.2, laser_max_dist 30, use_max_scan_range
+ * 20, z in (-1, 1), cutoff 30, identity transform); the caller sets angles and the transform. */
+void hs_default_laser(hs_laser *laser, int n_beams, float angle_min, float angle_increment);
+/* Install the scan geometry.  unit_vectors: 2*n_beams doubles (cos_i, sin_i) of
+ * angle_min + (double)i * angle_increment as laser_geometry caches them (getUnitVectors_), or NULL to
+ * compute them here with the host libm. */
+int hs_set_laser(hs_ctx *ctx, const hs_laser *laser, const double *unit_vectors);
+/* d_ranges float[count][range_stride] (device) -> d_xy float2 (stride xy_stride), d_n int per stream,
+ * d_origo float2 per stream (may be NULL): the DataContainer of each stream, points in map scale. */
+int hs_ingest_batch_device(hs_ctx *ctx, int count, const float *d_ranges, int range_stride, float *d_xy,
+                           int xy_stride, int *d_n, float *d_origo, void *hip_stream);
+/* scanCallback for a batch: ingest every stream's ranges into the context's own point buffers, then
+ * one HectorSlamProcessor::update per stream (as hs_step_batch_device; hints NULL = last pose). */
+int hs_step_ranges_batch_device(hs_ctx *ctx, int stream_begin, int count, const float *d_ranges, int range_stride,
+                                const float *d_hints, void *hip_stream);
+/* scanCallback for one stream from host ranges (the ROS drop-in entry point). */
+int hs_update_ranges(hs_ctx *ctx, int stream, const float *ranges, float pose_out[3], float cov_out[9],
+                     int *did_update_out);
+
 /* Copy poses (float3), covariances (float9), did-update flags and Σ cells traversed of the last
  * step (int64, Σ_levels Σ_valid rays (abs_da + 1)) for every stream.  Any pointer may be NULL. */
 int hs_get_poses(hs_ctx *ctx, float *poses_out, float *covs_out, int *did_update_out, int64_t *cells_traversed_out);

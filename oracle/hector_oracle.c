@@ -674,3 +674,60 @@ int ho_ray_cells(int sx, int sy, int x0, int y0, int x1, int y1, unsigned int *o
 float ho_det_sinf(float x) { return odm_sinf(x); }
 float ho_det_cosf(float x) { return odm_cosf(x); }
 float ho_det_expf(float x) { return odm_expf(x); }
+
+/* ---- scan ingest: LaserScan -> DataContainer ------------------------------------------------------
+ * HectorMappingRos::scanCallback (lesson4/src/hector_mapping/hector_slam.cc:186-198):
+ *   projector_.projectLaser(scan, laser_point_cloud_, 30.0)  -- laser_geometry (third party, absent
+ *   here, not vendored: PARITY UNPINNED for this step).  Restated from its published
+ *   LaserProjection::projectLaser_: unit vectors cos / sin(angle_min + (double)i * angle_increment) in
+ *   double (getUnitVectors_, cached per scan geometry), output = (double)range * unit, a point is kept
+ *   when range < range_cutoff && range >= range_min (range_cutoff < 0 -> range_max), Point32 x / y are
+ *   the double products rounded to float, z = 0.
+ * then rosPointCloudToDataContainer (hector_slam.cc:320-362), followed statement by statement:
+ *   origo = Vector2f(laserPos.x, laserPos.y) * scaleToMap                                   (:329)
+ *   dist_sqr = x*x + y*y (float); keep if sqr_min < dist_sqr < sqr_max                      (:334-336)
+ *   drop if x < 0 && dist_sqr < 0.5f                                                         (:338-341)
+ *   drop if dist_sqr > use_max_scan_range^2 (double comparison)                               (:344-345)
+ *   p = laserTransform * (x, y, z): tf dot products ((b0 x + b1 y) + b2 z) + origin, double   (:348)
+ *   z_laser = (float)(p.z - laserPos.z); keep if z_min < z_laser < z_max                      (:351-353)
+ *   add Vector2f((float)p.x, (float)p.y) * scaleToMap                                          (:356)
+ * Returns the number of points written to xy_out (order preserved). */
+void ho_unit_vectors(int n, float angle_min, float angle_increment, double *cs_out)
+{
+    for (int i = 0; i < n; ++i) {
+        const double a = (double)angle_min + (double)i * (double)angle_increment;
+        cs_out[2 * i] = cos(a);
+        cs_out[2 * i + 1] = sin(a);
+    }
+}
+
+int ho_ingest(int n, const float *ranges, const double *cs, double range_cutoff, float range_min, const double *tf,
+              float sqr_min, float sqr_max, double use_max, float z_min, float z_max, float scale, float *xy_out,
+              float *origo_out)
+{
+    origo_out[0] = (float)tf[9] * scale;
+    origo_out[1] = (float)tf[10] * scale;
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        const float range = ranges[i];
+        if (!((range < range_cutoff) && (range >= range_min))) continue;
+        const float x = (float)((double)range * cs[2 * i]);
+        const float y = (float)((double)range * cs[2 * i + 1]);
+        const float z = 0.0f;
+        const float dist_sqr = x * x + y * y;
+        if (!((dist_sqr > sqr_min) && (dist_sqr < sqr_max))) continue;
+        if ((x < 0.0f) && (dist_sqr < 0.50f)) continue;
+        if ((double)dist_sqr > use_max * use_max) continue;
+        const double vx = (double)x, vy = (double)y, vz = (double)z;
+        const double px = ((tf[0] * vx + tf[1] * vy) + tf[2] * vz) + tf[9];
+        const double py = ((tf[3] * vx + tf[4] * vy) + tf[5] * vz) + tf[10];
+        const double pz = ((tf[6] * vx + tf[7] * vy) + tf[8] * vz) + tf[11];
+        const float zl = (float)(pz - tf[11]);
+        if (zl > z_min && zl < z_max) {
+            xy_out[2 * m] = (float)px * scale;
+            xy_out[2 * m + 1] = (float)py * scale;
+            ++m;
+        }
+    }
+    return m;
+}

@@ -80,6 +80,9 @@ def hector_lib(variant: str = "") -> C.CDLL:
         L.ho_publish_level.argtypes = [_p, _i, _p]
         L.ho_ray_cells.restype = _i
         L.ho_ray_cells.argtypes = [_i, _i, _i, _i, _i, _i, _p, _i]
+        L.ho_unit_vectors.argtypes = [_i, _f, _f, _p]
+        L.ho_ingest.restype = _i
+        L.ho_ingest.argtypes = [_i, _p, _p, C.c_double, _f, _p, _f, _f, C.c_double, _f, _f, _f, _p, _p]
         for n in ("ho_det_sinf", "ho_det_cosf", "ho_det_expf"):
             getattr(L, n).restype = _f
             getattr(L, n).argtypes = [_f]
@@ -209,6 +212,28 @@ class HectorOracle:
         o = np.zeros((n, 16), np.float32)
         self.L.ho_get_trace(self.h, _fp(o))
         return o
+
+
+def unit_vectors(n, angle_min, angle_increment):
+    """laser_geometry getUnitVectors_ restated (ho_unit_vectors): [n, 2] double (cos, sin)."""
+    out = np.zeros((n, 2), dtype=np.float64)
+    hector_lib().ho_unit_vectors(n, angle_min, angle_increment, _fp(out))
+    return out
+
+
+def ingest(ranges, cs, laser: dict, scale_to_map: float):
+    """projectLaser + rosPointCloudToDataContainer restated (ho_ingest, hector_slam.cc:193, 320-362).
+    laser: range_cutoff, range_min, tf (12 doubles: basis row-major + origin), sqr_min, sqr_max,
+    use_max, z_min, z_max.  Returns (points float32 [m, 2], origo float32 [2])."""
+    r = np.ascontiguousarray(ranges, dtype=np.float32)
+    cs = np.ascontiguousarray(cs, dtype=np.float64)
+    tf = np.ascontiguousarray(laser["tf"], dtype=np.float64)
+    xy = np.zeros((r.shape[0], 2), dtype=np.float32)
+    org = np.zeros(2, dtype=np.float32)
+    m = hector_lib().ho_ingest(r.shape[0], _fp(r), _fp(cs), laser["range_cutoff"], laser["range_min"], _fp(tf),
+                               laser["sqr_min"], laser["sqr_max"], laser["use_max"], laser["z_min"], laser["z_max"],
+                               scale_to_map, _fp(xy), _fp(org))
+    return xy[:m].copy(), org
 
 
 def ray_cells(sx, sy, x0, y0, x1, y1):

@@ -1,0 +1,167 @@
+"""GPU parity of the on-device scan ingest:
+HectorMappingRos::scanCallback's projectLaser + rosPointCloudToDataContainer
+(lesson4/src/hector_mapping/hector_slam.cc:186-198, 320-362) as hs_ingest_kernel, against the C
+restatement oracle.ingest.  Bar: bit-exact (point count, every float bit of every point, origo).
+laser_geometry itself is absent (third party), so the projectLaser step is parity unpinned; the
+node-side filters are restated from the reference file line by line.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle as O
+from slam2d import synth
+from slam2d.hector import HectorFleet, HsLaser
+
+pytestmark = pytest.mark.gpu
+
+N = 1081
+AMIN = np.float32(-3.0 * math.pi / 4.0)
+AINC = np.float32(math.radians(0.25))
+
+
+def _roll_pi_laser(n=N):
+    """hector_slam.launch's static TF: x y z yaw pitch roll = 0 0 0.254 0 0 3.1415926."""
+    L = HsLaser.defaults(n, float(AMIN), float(AINC))
+    r = 3.1415926
+    c, s = math.cos(r), math.sin(r)
+    basis = [1.0, 0.0, 0.0, 0.0, c, -s, 0.0, s, c]
+    for i, v in enumerate(basis):
+        L.basis[i] = v
+    L.origin[0], L.origin[1], L.origin[2] = 0.0, 0.0, 0.254
+    return L
+
+
+def _tilted_laser(n=N):
+    """A pitched, offset laser: z of far points leaves (-1, 1), exercising the z filter (:351-353)."""
+    L = HsLaser.defaults(n, float(AMIN), float(AINC))
+    p = 0.08
+    c, s = math.cos(p), math.sin(p)
+    basis = [c, 0.0, s, 0.0, 1.0, 0.0, -s, 0.0, c]
+    for i, v in enumerate(basis):
+        L.basis[i] = v
+    L.origin[0], L.origin[1], L.origin[2] = 0.31, -0.07, 0.4
+    L.range_min = 0.05
+    return L
+
+
+def _edge_ranges(rng, B, n=N):
+    """Ranges hitting every branch: NaN / inf / negative, below range_min, around 0.2 m, the
+    x < 0 && d^2 < 0.5 cut (rear beams under 0.707 m), around 20 m and 30 m."""
+    r = rng.uniform(0.0, 32.0, size=(B, n)).astype(np.float32)
+    pick = rng.integers(0, 9, size=(B, n))
+    r[pick == 0] = np.nan
+    r[pick == 1] = np.inf
+    r[pick == 2] = rng.uniform(0.15, 0.25, size=int((pick == 2).sum())).astype(np.float32)
+    r[pick == 3] = rng.uniform(0.6, 0.8, size=int((pick == 3).sum())).astype(np.float32)
+    r[pick == 4] = rng.uniform(19.9, 20.1, size=int((pick == 4).sum())).astype(np.float32)
+    r[pick == 5] = rng.uniform(29.9, 30.1, size=int((pick == 5).sum())).astype(np.float32)
+    r[pick == 6] = -1.0
+    r[:, :8] = np.float32(30.0)   # exactly the cutoff: dropped (range < cutoff)
+    r[:, 8:16] = np.float32(20.0)
+    return r
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.int32)
+
+
+@pytest.mark.parametrize("make_laser", [_roll_pi_laser, _tilted_laser, None])
+def test_ingest_batch_bitexact(gpu, make_laser):
+    import torch
+    B = 64
+    L = make_laser() if make_laser else HsLaser.defaults(N, float(AMIN), float(AINC))
+    fleet = HectorFleet(B, 0.05, 256, (0.5, 0.5), 1, max_points=N)
+    fleet.set_laser(L)
+    rng = np.random.default_rng(4242)
+    r = _edge_ranges(rng, B)
+    d_r = torch.from_numpy(r).cuda()
+    d_xy = torch.full((B, N, 2), -7.0, dtype=torch.float32, device="cuda")
+    d_n = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    d_o = torch.zeros((B, 2), dtype=torch.float32, device="cuda")
+    fleet.ingest_device(B, d_r.data_ptr(), N, d_xy.data_ptr(), N, d_n.data_ptr(), d_o.data_ptr())
+    torch.cuda.synchronize()
+    xy, n, org = d_xy.cpu().numpy(), d_n.cpu().numpy(), d_o.cpu().numpy()
+    cs = O.unit_vectors(N, float(AMIN), float(AINC))
+    scale = fleet.scale_to_map()
+    total = 0
+    for b in range(B):
+        opts, oorg = O.ingest(r[b], cs, L.as_oracle_dict(), scale)
+        assert n[b] == opts.shape[0], (b, n[b], opts.shape[0])
+        assert np.array_equal(_bits(xy[b, : n[b]]), _bits(opts)), b
+        assert np.array_equal(_bits(org[b]), _bits(oorg))
+        assert np.all(xy[b, n[b]:] == -7.0), "ingest wrote past the stream's point count"
+        total += n[b]
+    assert 0 < total < B * N  # the filters dropped some beams and kept others
+
+
+def test_ingest_empty_and_all_invalid(gpu):
+    import torch
+    L = HsLaser.defaults(N, float(AMIN), float(AINC))
+    fleet = HectorFleet(2, 0.05, 256, (0.5, 0.5), 1, max_points=N)
+    fleet.set_laser(L)
+    r = np.full((2, N), np.nan, np.float32)
+    r[1] = 0.1  # all under laser_min_dist
+    d_r = torch.from_numpy(r).cuda()
+    d_xy = torch.zeros((2, N, 2), dtype=torch.float32, device="cuda")
+    d_n = torch.full((2,), -1, dtype=torch.int32, device="cuda")
+    fleet.ingest_device(2, d_r.data_ptr(), N, d_xy.data_ptr(), N, d_n.data_ptr())
+    torch.cuda.synchronize()
+    assert d_n.cpu().tolist() == [0, 0]
+    # an empty DataContainer: the step returns the hint (ScanMatcher.h:65, 96) and updates the map
+    pose, _, did = fleet.update_ranges(0, r[0])
+    assert np.all(pose == 0.0) and did
+
+
+def test_step_ranges_matches_oracle_pipeline(gpu):
+    """scanCallback end to end: raw ranges -> ingest -> update on the device, vs oracle.ingest ->
+    oracle process, 2 streams x 12 scans, 2 levels: poses, gate and maps bit-exact."""
+    import torch
+    S, T, LV, SIZE = 2, 12, 2, 512
+    scans = synth.make_streams(S, T, with_points=False)
+    L = _roll_pi_laser()
+    fleet = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(0.4, 0.9)
+    fleet.set_laser(L)
+    oras = [O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=256) for _ in range(S)]
+    for o in oras:
+        o.set_update_factors(0.4, 0.9)
+        o.set_thresholds(0.4, 0.9)
+    cs = O.unit_vectors(N, float(AMIN), float(AINC))
+    scale = fleet.scale_to_map()
+    for t in range(T):
+        r = np.ascontiguousarray(scans.ranges[:, t, :])
+        d_r = torch.from_numpy(r).cuda()
+        fleet.step_ranges_device(d_r.data_ptr(), N)
+        gp, _, gd, _ = fleet.poses()
+        for s in range(S):
+            pts, org = O.ingest(r[s], cs, L.as_oracle_dict(), scale)
+            op, _, od = oras[s].process(pts, origo=tuple(org))
+            assert gd[s] == od, (t, s)
+            assert np.array_equal(_bits(gp[s]), _bits(op)), (t, s, gp[s], op)
+    for s in range(S):
+        for lvl in range(LV):
+            m = fleet.get_map(s, lvl)
+            ol, ou = oras[s].level(lvl)
+            assert np.array_equal(m["upd"], ou)
+            assert np.array_equal(_bits(m["logodds"]), _bits(ol))
+
+
+def test_update_ranges_host_entry_equals_batch(gpu):
+    import torch
+    scans = synth.make_streams(1, 6, with_points=False)
+    L = _roll_pi_laser()
+    a = HectorFleet(1, 0.05, 256, (0.5, 0.5), 1, max_points=N)
+    b = HectorFleet(1, 0.05, 256, (0.5, 0.5), 1, max_points=N)
+    for f in (a, b):
+        f.set_laser(L)
+        f.set_thresholds(-1.0, -1.0)
+    for t in range(6):
+        r = np.ascontiguousarray(scans.ranges[0, t])
+        pa, _, _ = a.update_ranges(0, r)
+        d_r = torch.from_numpy(r[None]).cuda()
+        b.step_ranges_device(d_r.data_ptr(), N)
+        pb = b.poses()[0][0]
+        assert np.array_equal(_bits(pa), _bits(pb)), t

@@ -450,7 +450,9 @@ def run_karto(args, world, rank, dev):
     cfg = args.config
     M = args.matches or (512 if cfg == "karto" else 32)
     K, W = args.steps, args.warmup
-    lz, p, ranges, poses, query, beg, idx, NB, pen, ref = karto_setup(cfg, M, 777 + rank)
+    shard = args.karto_shard
+    # replicas: every rank its own matches; sharded: every rank the SAME matches, window split by angle
+    lz, p, ranges, poses, query, beg, idx, NB, pen, ref = karto_setup(cfg, M, 777 + (0 if shard else rank))
     S = ranges.shape[0]
     sm = karto.ScanMatcher(lz, p, max_matches=M, max_scans=S, max_base=NB)
     d_r = torch.from_numpy(ranges).to(dev)
@@ -461,8 +463,11 @@ def run_karto(args, world, rank, dev):
 
     def step():
         sm.set_scans_device(0, S, d_r.data_ptr(), d_p.data_ptr(), hip_stream=hs)
-        sm.match_batch_device(M, d_q.data_ptr(), d_b.data_ptr(), d_i.data_ptr(), d_res.data_ptr(), pen, ref,
-                              hip_stream=hs)
+        if shard:  # one RCCL all-reduce (MAX) of the window's exchange words per step
+            sm.match_sharded(M, d_q.data_ptr(), d_b.data_ptr(), d_i.data_ptr(), d_res.data_ptr(), pen, ref)
+        else:
+            sm.match_batch_device(M, d_q.data_ptr(), d_b.data_ptr(), d_i.data_ptr(), d_res.data_ptr(), pen, ref,
+                                  hip_stream=hs)
 
     for _ in range(W):
         step()
@@ -483,6 +488,8 @@ def run_karto(args, world, rank, dev):
     kt = sm.kernel_times(reset=True)
     res = karto.results_from_bytes(d_res.cpu().numpy())
     t_max, total = aggregate_over_ranks(elapsed, float(M * K), dev)
+    if shard:
+        total = float(M * K)  # the same matches on every rank: the job's matches, not the ranks' sum
     if rank == 0:
         cpu = None if (args.no_cpu_baseline or world > 1) else karto_cpu_baseline(cfg)
         info = sm.info
@@ -495,7 +502,8 @@ def run_karto(args, world, rank, dev):
             # plus the 16-byte local point and 1-byte flag each (angle, tile) workgroup reads per point
             tiles = -(-int(math.sqrt(npos)) // 16) ** 2
             pts = float(np.isfinite(ranges[query]).sum(axis=1).mean())
-            per_launch = M * (npos * nA * pts + nA * tiles * pts * 17.0)
+            nA_own = sum(1 for a in range(nA) if karto.shard_owns_angle(a, rank, world)) if shard else nA
+            per_launch = M * (npos * nA_own * pts + nA_own * tiles * pts * 17.0)
             avg_s = coarse_ms / coarse_n * 1e-3
             ach = per_launch / avg_s / 1e9
             roof = {"bound": "hbm", "kernel": "kt_coarse_kernel", "achieved": round(ach, 1), "peak": 8000.0,
@@ -505,10 +513,12 @@ def run_karto(args, world, rank, dev):
                             "are L2 / Infinity-Cache resident, so this is a gather rate, not DRAM traffic"}
         out = {"metric": KT_METRIC[cfg], "value": round(total / t_max, 1), "unit": "matches/s", "n_gpus": world,
                "steps": K, "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-               "config": {"workload": f"lesson6 karto_slam {cfg}: {M} independent MatchScan calls per GPU, "
+               "scaling": "strong" if shard else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+               "config": {"workload": f"lesson6 karto_slam {cfg}: {M} independent MatchScan calls "
+                                      f"{'per job, coarse window split over the GPUs by angle' if shard else 'per GPU'}, "
                                       f"{NB} base scans each, 1081 beams, grid {info['grid_size']}^2",
-                          "config": cfg, "matches_per_gpu": M, "parallelism": f"replicas x{world}",
+                          "config": cfg, "matches_per_gpu": M,
+                          "parallelism": f"window sharded x{world} (RCCL MAX all-reduce)" if shard else f"replicas x{world}",
                           "kernel_ms": {k: round(v[0], 3) for k, v in kt.items()}},
                "roofline": roof, "cpu_baseline": cpu,
                "ok_results": int((res["status"] == 0).sum())}
@@ -530,6 +540,8 @@ def main():
     ap.add_argument("--pairs", type=int, default=2048, help="plicp: scan pairs per GPU per step")
     ap.add_argument("--matches", type=int, default=0, help="karto: MatchScan calls per GPU per step (0 = default)")
     ap.add_argument("--particles", type=int, default=1024, help="gmapping: particles of the whole job")
+    ap.add_argument("--karto-shard", action="store_true",
+                    help="karto: split every match's coarse window over the GPUs (one RCCL all-reduce per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--no-copy-probe", action="store_true", help="skip the copy-bandwidth probe")

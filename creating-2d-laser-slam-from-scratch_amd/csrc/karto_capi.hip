@@ -48,6 +48,7 @@ struct kt_ctx {
     KtGeom g{};
     int max_matches = 0, max_scans = 0, max_base = 0;
     int slots = 0;  // match slots resident at once (kt_run_batch chunk)
+    bool sharded_binned = false;  // AddScans variant of the last kt_match_sharded_begin_device
     int build_per_match = 1;  // CAS AddScans: one workgroup per match (1) or per (match, base scan) (0)
     int binned = 0;           // AddScans by kt_addscans_kernel (tile-binned, plain stores)
     int *d_scratch = nullptr, *d_dirty = nullptr, *d_dirty_cnt = nullptr;
@@ -195,15 +196,16 @@ int kt_prepare(kt_ctx *c, int first, int count, hipStream_t s)
     return KT_OK;
 }
 
-int kt_run_chunk(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, const int *d_bidx, int penalize,
-                 int refine, kt_result *d_res, hipStream_t s)
+// MatchScan steps 1-5 for a chunk: centre the grids (kt_begin_kernel) and AddScans
+int kt_chunk_build(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, const int *d_bidx, hipStream_t s,
+                   bool &binned)
 {
     const KtGeom &g = c->g;
     const int groups = (count + 7) / 8;
     KT_LAUNCH(K_BEGIN, kt_begin_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->pool(), d_query, c->d_state,
               c->d_posmax);
     // the binned AddScans runs one workgroup per match: small batches use the per-(match, base scan) kernel
-    const bool binned = c->binned && count >= 128;
+    binned = c->binned && count >= 128;
     const bool per_match = !binned && c->build_per_match && count >= 128;
     if (c->max_base > 0) {
         if (binned)
@@ -217,14 +219,25 @@ int kt_run_chunk(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, co
             KT_LAUNCH(K_BUILD, (kt_build_kernel<0, 4>), dim3(groups * 8 * c->max_base), dim3(KT_THREADS), 0, s, g,
                       c->pool(), c->d_state, d_bbeg, d_bidx, c->d_kernel, c->d_grids, count, c->max_base);
     }
-    for (int pass = 0; pass < g.npass; ++pass) {
-        const long long blocks = (long long)groups * 8 * g.nang[pass] * g.tiles * g.tiles;
-        if (blocks > 0x7fffffffLL) return kfail(KT_EINVAL, "coarse launch too large: lower the batch size");
-        KT_LAUNCH(K_COARSE, kt_coarse_kernel, dim3((unsigned)blocks), dim3(KT_THREADS), (size_t)g.n * sizeof(int), s,
-                  g, c->pool(), c->d_state, c->d_grids, c->d_resp, c->d_posmax, count, pass, penalize);
-        KT_LAUNCH(K_SELECT, kt_select_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->d_state, c->d_resp,
-                  c->d_posmax, c->d_tie_idx, c->d_tie_val, pass, refine, d_res);
-    }
+    return KT_OK;
+}
+
+int kt_chunk_coarse(kt_ctx *c, int count, int pass, int penalize, int shard, int nshards, hipStream_t s)
+{
+    const KtGeom &g = c->g;
+    const long long blocks = (long long)((count + 7) / 8) * 8 * g.nang[pass] * g.tiles * g.tiles;
+    if (blocks > 0x7fffffffLL) return kfail(KT_EINVAL, "coarse launch too large: lower the batch size");
+    KT_LAUNCH(K_COARSE, kt_coarse_kernel, dim3((unsigned)blocks), dim3(KT_THREADS), (size_t)g.n * sizeof(int), s, g,
+              c->pool(), c->d_state, c->d_grids, c->d_resp, c->d_posmax, count, pass, penalize, shard, nshards);
+    return KT_OK;
+}
+
+// the fine match (MatchScan step 7) and the grids' footprint clear
+int kt_chunk_finish(kt_ctx *c, int count, const int *d_bbeg, const int *d_bidx, int penalize, int refine,
+                    kt_result *d_res, hipStream_t s, bool binned)
+{
+    const KtGeom &g = c->g;
+    const int groups = (count + 7) / 8;
     if (refine)
         KT_LAUNCH(K_FINE, kt_fine_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->pool(), c->d_state, c->d_grids,
                   penalize, d_res);
@@ -235,6 +248,20 @@ int kt_run_chunk(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, co
         KT_LAUNCH(K_CLEAR, (kt_build_kernel<1, 4>), dim3(groups * 8 * c->max_base), dim3(KT_THREADS), 0, s, g,
                   c->pool(), c->d_state, d_bbeg, d_bidx, c->d_kernel, c->d_grids, count, c->max_base);
     return KT_OK;
+}
+
+int kt_run_chunk(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, const int *d_bidx, int penalize,
+                 int refine, kt_result *d_res, hipStream_t s)
+{
+    bool binned = false;
+    int rc = kt_chunk_build(c, count, d_query, d_bbeg, d_bidx, s, binned);
+    if (rc != KT_OK) return rc;
+    for (int pass = 0; pass < c->g.npass; ++pass) {
+        if ((rc = kt_chunk_coarse(c, count, pass, penalize, 0, 1, s)) != KT_OK) return rc;
+        KT_LAUNCH(K_SELECT, kt_select_kernel, dim3(count), dim3(KT_THREADS), 0, s, c->g, c->d_state, c->d_resp,
+                  c->d_posmax, c->d_tie_idx, c->d_tie_val, pass, refine, d_res);
+    }
+    return kt_chunk_finish(c, count, d_bbeg, d_bidx, penalize, refine, d_res, s, binned);
 }
 
 // The batch runs in chunks of `slots` matches (default: all of them).  Smaller chunks keep a chunk's
@@ -478,6 +505,49 @@ int kt_match_scan(kt_ctx *c, const double *q_ranges, const double q_pose[3], int
     KCHK(hipMemcpyAsync(result, c->d_res, sizeof(kt_result), hipMemcpyDeviceToHost, s));
     KCHK(hipStreamSynchronize(s));
     return KT_OK;
+}
+
+size_t kt_window_exchange_words(kt_ctx *c)
+{
+    if (!c) return 0;
+    const size_t nxy2 = (size_t)c->g.nxy * c->g.nxy;
+    return 2 + nxy2 + nxy2 * (size_t)c->g.nang[0];
+}
+
+int kt_match_sharded_begin_device(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, const int *d_bidx,
+                                  int do_penalize, int shard, int nshards, int64_t *d_exchange, void *hip_stream)
+{
+    if (!c || !d_query || !d_bbeg || !d_exchange) return kfail(KT_EINVAL, "NULL argument");
+    if (count < 1 || count > c->slots) return kfail(KT_EINVAL, "sharded batch must hold 1 .. slots matches");
+    if (nshards < 1 || shard < 0 || shard >= nshards) return kfail(KT_EINVAL, "need 0 <= shard < nshards");
+    if (c->g.npass != 1) return kfail(KT_EINVAL, "a sharded window does not support response expansion");
+    if (c->max_base > 0 && !d_bidx) return kfail(KT_EINVAL, "d_base_index is NULL");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    bool binned = false;
+    int rc = kt_chunk_build(c, count, d_query, d_bbeg, d_bidx, s, binned);
+    if (rc != KT_OK) return rc;
+    c->sharded_binned = binned;
+    if ((rc = kt_chunk_coarse(c, count, 0, do_penalize ? 1 : 0, shard, nshards, s)) != KT_OK) return rc;
+    hipLaunchKernelGGL(kt_exchange_kernel, dim3(count), dim3(KT_THREADS), 0, s, c->g, c->d_state, c->d_resp,
+                       c->d_posmax, (long long *)d_exchange, 0);
+    KCHK(hipGetLastError());
+    return KT_OK;
+}
+
+int kt_match_sharded_end_device(kt_ctx *c, int count, const int *d_bbeg, const int *d_bidx, int do_penalize,
+                                int do_refine, const int64_t *d_exchange, kt_result *d_res, void *hip_stream)
+{
+    if (!c || !d_bbeg || !d_exchange || !d_res) return kfail(KT_EINVAL, "NULL argument");
+    if (count < 1 || count > c->slots) return kfail(KT_EINVAL, "sharded batch must hold 1 .. slots matches");
+    if (c->max_base > 0 && !d_bidx) return kfail(KT_EINVAL, "d_base_index is NULL");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipLaunchKernelGGL(kt_exchange_kernel, dim3(count), dim3(KT_THREADS), 0, s, c->g, c->d_state, c->d_resp,
+                       c->d_posmax, (long long *)d_exchange, 1);
+    KCHK(hipGetLastError());
+    KT_LAUNCH(K_SELECT, kt_select_kernel, dim3(count), dim3(KT_THREADS), 0, s, c->g, c->d_state, c->d_resp,
+              c->d_posmax, c->d_tie_idx, c->d_tie_val, 0, do_refine ? 1 : 0, d_res);
+    return kt_chunk_finish(c, count, d_bbeg, d_bidx, do_penalize ? 1 : 0, do_refine ? 1 : 0, d_res, s,
+                           c->sharded_binned);
 }
 
 int kt_set_timing(kt_ctx *c, int enable)

@@ -779,7 +779,7 @@ kt_clear_tiles_kernel(KtGeom g, unsigned char *grids, const int *__restrict__ di
 // =================================================================================================
 __global__ void __launch_bounds__(KT_THREADS)
 kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict__ grids, double *resp,
-                 unsigned long long *posmax, int count, int pass, int penalize)
+                 unsigned long long *posmax, int count, int pass, int penalize, int shard, int nshards)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char kt_smem[];
     int *soff = reinterpret_cast<int *>(kt_smem);  // [npts]
@@ -800,6 +800,9 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
     const int a = w / T2, t = w - a * T2;
     const int ty = t / g.tiles, tx = t - ty * g.tiles;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // window sharded over GPUs (kt_match_sharded_begin_device): this rank owns the angles
+    // a = shard (mod nshards); the others' responses are left +0.0 for the MAX all-reduce
+    const bool owned = (a % nshards) == shard;
 
     const double cxs = S.center[0], cys = S.center[1], chs = S.center[2];
     const double gox = S.gox, goy = S.goy;
@@ -810,7 +813,7 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
     const int q = S.query, npts = S.npts;
     const double2 *loc = P.loc + (size_t)q * g.n;
     const unsigned char *bad = P.bad + (size_t)q * g.n;
-    for (int k = tid; k < npts; k += KT_THREADS) {
+    for (int k = tid; owned && k < npts; k += KT_THREADS) {
         int o = KT_INVALID;
         if (!bad[k]) {
             const double2 l = loc[k];
@@ -845,6 +848,13 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
                 if (gpos[j] != gpos[0] + 2 * j) fast = false;
             }
         }
+    }
+    if (!owned) {  // block-uniform
+        const int pl = tid >> 2, pj = tid & 3;
+        const int piy = ty * KT_TILE + (pl >> 2);
+        const int pix = tx * KT_TILE + (pl & 3) * 4 + pj;
+        if (piy < g.nxy && pix < g.nxy) resp[(size_t)m * g.max_poses + ((size_t)piy * g.nxy + pix) * nA + a] = 0.0;
+        return;
     }
     __syncthreads();
     const unsigned ds = (unsigned)g.data_size;
@@ -953,6 +963,39 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
     if (tid == 0) {
         const double bb = kt_max(kt_max(sbest[0], sbest[1]), kt_max(sbest[2], sbest[3]));
         atomicMax(&S.best_bits, kt_bits(bb));
+    }
+}
+
+// =================================================================================================
+// kt_exchange_kernel: the per-match state a sharded window exchanges (dir 0: export, 1: import)
+//   x[m] = [best bits, ERANGE flag, posmax (nxy^2 bits), responses (nxy^2 * nA bits)]
+// every value is a non-negative double, so the int64 MAX all-reduce of the ranks' exports is exactly
+// the union of their angles (non-owned responses are +0.0, posmax / best are maxima already).
+// =================================================================================================
+__global__ void __launch_bounds__(KT_THREADS)
+kt_exchange_kernel(KtGeom g, KtState *st, double *resp, unsigned long long *posmax, long long *xbuf, int dir)
+{
+    const int m = blockIdx.x, tid = threadIdx.x;
+    KtState &S = st[m];
+    const int nxy2 = g.nxy * g.nxy;
+    const int np = nxy2 * g.nang[0];
+    long long *x = xbuf + (size_t)m * (2 + nxy2 + np);
+    unsigned long long *pm = posmax + (size_t)m * nxy2;
+    long long *r = reinterpret_cast<long long *>(resp + (size_t)m * g.max_poses);
+    if (dir == 0) {
+        if (tid == 0) {
+            x[0] = (long long)S.best_bits;
+            x[1] = S.status == KT_ERANGE ? 1 : 0;
+        }
+        for (int i = tid; i < nxy2; i += KT_THREADS) x[2 + i] = (long long)pm[i];
+        for (int i = tid; i < np; i += KT_THREADS) x[2 + nxy2 + i] = r[i];
+    } else {
+        if (tid == 0) {
+            S.best_bits = (unsigned long long)x[0];
+            if (x[1]) S.status = KT_ERANGE;
+        }
+        for (int i = tid; i < nxy2; i += KT_THREADS) pm[i] = (unsigned long long)x[2 + i];
+        for (int i = tid; i < np; i += KT_THREADS) r[i] = x[2 + nxy2 + i];
     }
 }
 

@@ -58,6 +58,10 @@ def _declare(L):
     L.kt_set_scans_device.argtypes = [vp, i, i, vp, vp, vp]
     L.kt_match_scan.argtypes = [vp, vp, vp, i, vp, vp, i, i, C.POINTER(KtResult)]
     L.kt_match_batch_device.argtypes = [vp, i, vp, vp, vp, i, i, vp, vp]
+    L.kt_window_exchange_words.restype = C.c_size_t
+    L.kt_window_exchange_words.argtypes = [vp]
+    L.kt_match_sharded_begin_device.argtypes = [vp, i, vp, vp, vp, i, i, i, vp, vp]
+    L.kt_match_sharded_end_device.argtypes = [vp, i, vp, vp, i, i, vp, vp, vp]
     L.kt_set_timing.argtypes = [vp, i]
     L.kt_kernel_name.restype = C.c_char_p
     L.kt_kernel_name.argtypes = [i]
@@ -154,6 +158,45 @@ class ScanMatcher:
                                                  C.c_void_p(d_results), C.c_void_p(hip_stream or None)),
                     "kt_match_batch_device")
 
+    # ---- one window sharded over GPUs ----
+    def exchange_words(self) -> int:
+        """int64 words one match exports in a sharded window (kt_window_exchange_words)."""
+        return int(self.L.kt_window_exchange_words(self.h))
+
+    def match_sharded_begin_device(self, count: int, d_query: int, d_base_begin: int, d_base_index: int,
+                                   shard: int, nshards: int, d_exchange: int, doPenalize: bool = True,
+                                   hip_stream: int = 0):
+        self._check(self.L.kt_match_sharded_begin_device(self.h, count, C.c_void_p(d_query), C.c_void_p(d_base_begin),
+                                                         C.c_void_p(d_base_index), int(doPenalize), shard, nshards,
+                                                         C.c_void_p(d_exchange), C.c_void_p(hip_stream or None)),
+                    "kt_match_sharded_begin_device")
+
+    def match_sharded_end_device(self, count: int, d_base_begin: int, d_base_index: int, d_exchange: int,
+                                 d_results: int, doPenalize: bool = True, doRefineMatch: bool = True,
+                                 hip_stream: int = 0):
+        self._check(self.L.kt_match_sharded_end_device(self.h, count, C.c_void_p(d_base_begin),
+                                                       C.c_void_p(d_base_index), int(doPenalize), int(doRefineMatch),
+                                                       C.c_void_p(d_exchange), C.c_void_p(d_results),
+                                                       C.c_void_p(hip_stream or None)),
+                    "kt_match_sharded_end_device")
+
+    def match_sharded(self, count: int, d_query: int, d_base_begin: int, d_base_index: int, d_results: int,
+                      doPenalize: bool = True, doRefineMatch: bool = True, group=None):
+        """MatchScan batch with the coarse window split over the ranks of `group` (one GPU each): every
+        rank evaluates the angles a = rank (mod world), ONE all-reduce (MAX) of the exchange words over
+        RCCL, then every rank finishes the identical result (equal to match_batch_device)."""
+        import torch
+        import torch.distributed as dist
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        hs = torch.cuda.current_stream().cuda_stream
+        x = torch.empty((count, self.exchange_words()), dtype=torch.int64, device="cuda")
+        self.match_sharded_begin_device(count, d_query, d_base_begin, d_base_index, rank, world, x.data_ptr(),
+                                        doPenalize, hs)
+        allreduce_window(x, group)
+        self.match_sharded_end_device(count, d_base_begin, d_base_index, x.data_ptr(), d_results, doPenalize,
+                                      doRefineMatch, hs)
+
     def set_timing(self, on: bool):
         self._check(self.L.kt_set_timing(self.h, 1 if on else 0), "kt_set_timing")
 
@@ -164,6 +207,21 @@ class ScanMatcher:
         self._check(self.L.kt_get_kernel_times(self.h, ms.ctypes.data_as(C.c_void_p), n.ctypes.data_as(C.c_void_p),
                                                1 if reset else 0), "kt_get_kernel_times")
         return {self.L.kt_kernel_name(i).decode(): (float(ms[i]), int(n[i])) for i in range(k)}
+
+
+def shard_owns_angle(a: int, shard: int, nshards: int) -> bool:
+    """The coarse angle ownership rule of a sharded window (kt_coarse_kernel)."""
+    return a % nshards == shard
+
+
+def allreduce_window(x, group=None):
+    """The one exchange step of a sharded window: element-wise MAX over the ranks of the int64 export
+    words.  Every word is the bit pattern of a non-negative double (or a 0/1 flag), where signed-integer
+    order equals numeric order, so MAX of one owner's value and the others' +0.0 is that value."""
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(x, op=dist.ReduceOp.MAX, group=group)
+    return x
 
 
 def results_from_bytes(buf: np.ndarray) -> np.ndarray:

@@ -112,6 +112,25 @@ int kt_match_batch_device(kt_ctx *ctx, int count, const int *d_query, const int 
                           const int *d_base_index, int do_penalize, int do_refine, kt_result *d_results,
                           void *hip_stream);
 
+/* ONE batch of MatchScan calls with the coarse window split over nshards GPUs: one
+ * process per GPU, every rank passing the same pooled scans and arguments.  Phase 1 builds the
+ * correlation grids and evaluates the coarse responses of the angles a = shard (mod nshards)
+ * (CorrelateScan's pose loop, Mapper.cpp:371-425), then exports per match
+ *   [best, ERANGE flag, per-position max over angles, every pose's response]
+ * as int64 words (d_exchange: int64[count][kt_window_exchange_words(ctx)], caller-owned device memory;
+ * all values are non-negative doubles, non-owned responses +0.0).  The caller all-reduces d_exchange
+ * with MAX over the ranks (RCCL over xGMI), then phase 2 imports it and finishes the reference
+ * sequence: best, tie average in pose order, positional covariance (Mapper.cpp:427-523), fine match.
+ * Every rank ends with the identical result, bit-equal to kt_match_batch_device.  Requires
+ * count <= the context's slots and no response expansion (KT_EINVAL otherwise). */
+size_t kt_window_exchange_words(kt_ctx *ctx);
+int kt_match_sharded_begin_device(kt_ctx *ctx, int count, const int *d_query, const int *d_base_begin,
+                                  const int *d_base_index, int do_penalize, int shard, int nshards,
+                                  int64_t *d_exchange, void *hip_stream);
+int kt_match_sharded_end_device(kt_ctx *ctx, int count, const int *d_base_begin, const int *d_base_index,
+                                int do_penalize, int do_refine, const int64_t *d_exchange, kt_result *d_results,
+                                void *hip_stream);
+
 int kt_set_timing(kt_ctx *ctx, int enable);
 /* Accumulated device time per kernel: names kt_kernel_name(i), i < kt_num_kernels(). */
 int kt_num_kernels(void);

@@ -206,6 +206,7 @@ typedef struct {
     int lookup_cap;
     int n_angles, npts;
     int error;
+    double *dump_resp;  /* test hook: the first coarse CorrelateScan's responses in pose order */
 } ko_matcher;
 
 static void ko_w2g(const ko_matcher *m, double x, double y, double ox, double oy, int *gx, int *gy)
@@ -494,6 +495,10 @@ static double ko_correlate(ko_matcher *m, const ko_scan *s, const double center[
             }
         }
     }
+    if (!fine && m->dump_resp) {
+        for (size_t i = 0; i < np; i++) m->dump_resp[i] = pr[i].r;
+        m->dump_resp = NULL;
+    }
     double best = -1;
     for (size_t i = 0; i < np; i++) {
         best = ko_max(best, pr[i].r);
@@ -543,13 +548,14 @@ static double ko_correlate(ko_matcher *m, const ko_scan *s, const double center[
 
 /* ScanMatcher::MatchScan (Mapper.cpp:184-300).  Returns 0 or a negative error
  * (-1/-2/-3 parameters / memory, -4 an index the reference would have thrown on). */
-int ko_match_scan(const ko_laser *L, const ko_params *p, const double *q_ranges, const double q_pose[3], int n_base,
-                  const double *b_ranges, const double *b_poses, int do_penalize, int do_refine, double mean[3],
-                  double cov[9], double *response)
+static int ko_match_scan_ex(const ko_laser *L, const ko_params *p, const double *q_ranges, const double q_pose[3],
+                            int n_base, const double *b_ranges, const double *b_poses, int do_penalize, int do_refine,
+                            double mean[3], double cov[9], double *response, double *dump_resp)
 {
     ko_matcher m;
     memset(&m, 0, sizeof(m));
     m.p = p;
+    m.dump_resp = dump_resp;
     int rc = ko_geom_init(p, L, &m.g);
     if (rc) return rc;
     for (int i = 0; i < 9; i++) cov[i] = 0.0;
@@ -622,6 +628,24 @@ out:
     free(m.lookup);
     free(m.g.kernel);
     return rc;
+}
+
+int ko_match_scan(const ko_laser *L, const ko_params *p, const double *q_ranges, const double q_pose[3], int n_base,
+                  const double *b_ranges, const double *b_poses, int do_penalize, int do_refine, double mean[3],
+                  double cov[9], double *response)
+{
+    return ko_match_scan_ex(L, p, q_ranges, q_pose, n_base, b_ranges, b_poses, do_penalize, do_refine, mean, cov,
+                            response, NULL);
+}
+
+/* Test hook: the coarse window's responses (nY * nX * nAngles doubles, CorrelateScan's pose order
+ * y, x, angle, Mapper.cpp:371-425) of one MatchScan, for the sharded-window exchange tests. */
+int ko_coarse_responses(const ko_laser *L, const ko_params *p, const double *q_ranges, const double q_pose[3],
+                        int n_base, const double *b_ranges, const double *b_poses, int do_penalize, double *resp_out)
+{
+    double mean[3], cov[9], r;
+    return ko_match_scan_ex(L, p, q_ranges, q_pose, n_base, b_ranges, b_poses, do_penalize, 0, mean, cov, &r,
+                            resp_out);
 }
 
 /* The correlation grid AddScans builds for a query pose (test hook: compared with the device grid). */

@@ -392,6 +392,8 @@ def karto_lib():
         L.ko_grid_info.argtypes = [C.POINTER(KtParams), C.POINTER(KtLaser), _p]
         L.ko_kernel.restype = _i
         L.ko_kernel.argtypes = [C.POINTER(KtParams), C.POINTER(KtLaser), _p, _i]
+        L.ko_coarse_responses.restype = _i
+        L.ko_coarse_responses.argtypes = [C.POINTER(KtLaser), C.POINTER(KtParams), _p, _p, _i, _p, _p, _i, _p]
         L.ko_build_grid.restype = _i
         L.ko_build_grid.argtypes = [C.POINTER(KtLaser), C.POINTER(KtParams), _p, _i, _p, _p, _p]
         _KO = L
@@ -422,6 +424,21 @@ def karto_match(laser: KtLaser, params: KtParams, q_ranges, q_pose, b_ranges, b_
     if rc:
         raise RuntimeError(f"ko_match_scan: {rc}")
     return mean, cov.reshape(3, 3), r.value
+
+
+def karto_coarse_responses(laser: KtLaser, params: KtParams, q_ranges, q_pose, b_ranges, b_poses, n_xy: int,
+                           n_angles: int, penalize=True) -> np.ndarray:
+    """The first coarse CorrelateScan's responses [n_xy, n_xy, n_angles] in pose order (test hook)."""
+    q = np.ascontiguousarray(q_ranges, np.float64)
+    qp = np.ascontiguousarray(q_pose, np.float64)
+    b = np.ascontiguousarray(b_ranges, np.float64).reshape(-1, laser.n_readings)
+    bp = np.ascontiguousarray(b_poses, np.float64).reshape(-1, 3)
+    out = np.full(n_xy * n_xy * n_angles, np.nan, np.float64)
+    rc = karto_lib().ko_coarse_responses(C.byref(laser), C.byref(params), _fp(q), _fp(qp), b.shape[0], _fp(b),
+                                         _fp(bp), int(penalize), _fp(out))
+    if rc:
+        raise RuntimeError(f"ko_coarse_responses: {rc}")
+    return out.reshape(n_xy, n_xy, n_angles)
 
 
 def karto_build_grid(laser: KtLaser, params: KtParams, q_pose, b_ranges, b_poses) -> np.ndarray:

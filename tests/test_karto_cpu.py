@@ -91,3 +91,62 @@ def test_kt_create_rejects_unsupported_params():
     assert L.kt_create(C.byref(h), C.byref(lz), C.byref(bad), 1, 4, 3) == -1
     p = karto.default_params()
     assert p.search_size == 0.3 and p.resolution == 0.01 and abs(p.coarse_search_angle_offset - 20 * D) < 1e-15
+
+
+# ----------------------------------------------------------------------------- sharded window (gloo)
+def _window_case():
+    lz = laser()
+    p = params(loop=True)
+    p.search_size = 2.0  # 21 x 21 coarse positions x 21 angles
+    QR, qp, _, CR, CP = synth.karto_loop(1, 4, seed=31, perturb=(0.2, 0.2, 0.03))
+    resp = O.karto_coarse_responses(lz, p, QR[0], qp[0], CR[0], CP[0], 21, 21, penalize=True)
+    return resp
+
+
+def _window_worker(rank, world, port, out):
+    import os
+    import torch
+    import torch.distributed as dist
+
+    from slam2d import karto
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    resp = _window_case()
+    nA = resp.shape[2]
+    mine = resp.copy()
+    for a in range(nA):  # what this rank's kt_coarse_kernel leaves: other ranks' angles +0.0
+        if not karto.shard_owns_angle(a, rank, world):
+            mine[:, :, a] = 0.0
+    posmax = mine.max(axis=2)
+    best = mine.max()
+    x = torch.from_numpy(np.concatenate([[best], posmax.ravel(), mine.ravel()]).view(np.int64).copy())
+    karto.allreduce_window(x)
+    out[rank] = x.numpy().tobytes()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_window_exchange_gloo(world):
+    """the exchange step of a Karto window split over ranks by angle (the same
+    slam2d.karto.allreduce_window the GPU path calls, here over gloo): after the int64 MAX all-reduce
+    every rank holds, bit for bit, the unsharded window's responses, per-position maxima and best --
+    the inputs of the tie average and covariance, which then run identically on every rank."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_window_worker, args=(world, port, out), nprocs=world, join=True)
+        res = dict(out)
+    resp = _window_case()
+    assert np.all(resp >= 0.0) and resp.max() > 0.0
+    want = np.concatenate([[resp.max()], resp.max(axis=2).ravel(), resp.ravel()])
+    for r in range(world):
+        got = np.frombuffer(res[r], np.float64)
+        assert np.array_equal(got.view(np.int64), want.view(np.int64)), r

@@ -164,3 +164,87 @@ def test_batch_device_loop_window(gpu):
         o = O.karto_match(_olaser(lz), _oparams(p), QR[i], qp[i], CR[i], CP[i], False, False)
         assert out["status"][i] == 0
         _same((out["mean"][i], out["covariance"][i].reshape(3, 3), out["response"][i]), o)
+
+
+def _sharded_setup(lz, p, M, K, seed):
+    QR, qp, qt, CR, CP = synth.karto_loop(M, K, seed=seed, perturb=(0.2, 0.2, 0.03))
+    return QR, qp, CR, CP
+
+
+@pytest.mark.parametrize("loop,nshards,penalize,refine,M", [(True, 2, False, False, 4), (True, 3, True, True, 4),
+                                                             (False, 8, True, True, 6), (False, 2, True, True, 130)])
+def test_sharded_window_equals_unsharded(gpu, loop, nshards, penalize, refine, M):
+    """one batch with the coarse window split over `nshards` ranks (angles
+    a = shard mod nshards), the exchange words combined by element-wise MAX exactly as the RCCL
+    all-reduce does, then every shard's phase 2: identical results on every shard, bit-equal to the
+    unsharded kt_match_batch_device (and so to the oracle).  Emulated on one GPU with one context per
+    shard; the multi-process exchange itself is covered with gloo in tests/test_karto_cpu.py."""
+    import torch
+
+    lz = _laser()
+    p = karto.default_params(loop=loop)
+    if loop:
+        p.search_size = 2.0
+    K = 5
+    QR, qp, CR, CP = _sharded_setup(lz, p, M, K, seed=23 + M)
+    pr = torch.tensor(np.concatenate([QR, CR.reshape(-1, synth.N_BEAMS)]), dtype=torch.float64, device="cuda")
+    pp = torch.tensor(np.concatenate([qp, CP.reshape(-1, 3)]), dtype=torch.float64, device="cuda")
+    q = torch.arange(M, dtype=torch.int32, device="cuda")
+    beg = torch.arange(M + 1, dtype=torch.int32, device="cuda") * K
+    idx = torch.arange(M, M + M * K, dtype=torch.int32, device="cuda")
+    nbytes = M * C.sizeof(karto.KtResult)
+
+    def ctx():
+        sm = karto.ScanMatcher(lz, p, max_matches=M, max_scans=M * (K + 1), max_base=K)
+        sm.set_scans_device(0, M * (K + 1), pr.data_ptr(), pp.data_ptr())
+        return sm
+
+    ref = ctx()
+    r0 = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    ref.match_batch_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), r0.data_ptr(), penalize, refine)
+    shards = [ctx() for _ in range(nshards)]
+    words = shards[0].exchange_words()
+    xs = [torch.full((M, words), -1, dtype=torch.int64, device="cuda") for _ in range(nshards)]
+    for k, sm in enumerate(shards):
+        sm.match_sharded_begin_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), k, nshards, xs[k].data_ptr(),
+                                      penalize)
+    torch.cuda.synchronize()
+    assert all(bool((x >= 0).all()) for x in xs), "every exchange word is written and non-negative"
+    x = xs[0].clone()
+    for k in range(1, nshards):
+        x = torch.maximum(x, xs[k])
+    outs = []
+    for sm in shards:
+        r = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+        sm.match_sharded_end_device(M, beg.data_ptr(), idx.data_ptr(), x.data_ptr(), r.data_ptr(), penalize, refine)
+        outs.append(r)
+    torch.cuda.synchronize()
+    want = r0.cpu().numpy()
+    for r in outs:
+        assert np.array_equal(r.cpu().numpy(), want)
+    res = karto.results_from_bytes(want)
+    o = O.karto_match(_olaser(lz), _oparams(p), QR[0], qp[0], CR[0], CP[0], penalize, refine)
+    _same((res["mean"][0], res["covariance"][0].reshape(3, 3), res["response"][0]), o)
+    # a context reused after the sharded path: the grids were cleared
+    r2 = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    shards[0].match_batch_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), r2.data_ptr(), penalize, refine)
+    torch.cuda.synchronize()
+    assert np.array_equal(r2.cpu().numpy(), want)
+
+
+def test_sharded_rejects_expansion_and_bad_shard(gpu):
+    import torch
+    lz = _laser()
+    p = karto.default_params()
+    p.use_response_expansion = 1
+    sm = karto.ScanMatcher(lz, p, max_matches=1, max_scans=2, max_base=1)
+    x = torch.zeros((1, sm.exchange_words()), dtype=torch.int64, device="cuda")
+    q = torch.zeros(1, dtype=torch.int32, device="cuda")
+    beg = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
+    idx = torch.ones(1, dtype=torch.int32, device="cuda")
+    with pytest.raises(karto.Slam2dError):
+        sm.match_sharded_begin_device(1, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), 0, 2, x.data_ptr())
+    p.use_response_expansion = 0
+    sm2 = karto.ScanMatcher(lz, p, max_matches=1, max_scans=2, max_base=1)
+    with pytest.raises(karto.Slam2dError):
+        sm2.match_sharded_begin_device(1, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), 2, 2, x.data_ptr())

@@ -114,7 +114,7 @@ def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
     return 2.0 * nbytes * reps / dt / 1e9
 
 
-def cpu_baseline(cfg, seconds=10.0, seconds_o0=4.0):
+def cpu_baseline(cfg, seconds=10.0, seconds_o0=4.0, thresholds=(-1.0, -1.0)):
     """Time the CPU oracle (C restatement at -O3, reference sequential order, 1 core, exactly one
     stream as the reference node runs) on a bounded sample of the same workload: one stream,
     consecutive scans, forced map update each scan.  The -O0 build (the reference ships Debug,
@@ -129,7 +129,7 @@ def cpu_baseline(cfg, seconds=10.0, seconds_o0=4.0):
     def run(variant, budget):
         h = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0, lib_variant=variant)
         h.set_update_factors(0.4, 0.9)
-        h.set_thresholds(-1.0, -1.0)
+        h.set_thresholds(*thresholds)
         done = 0
         t0 = time.perf_counter()
         while done < n_scans and time.perf_counter() - t0 < budget:
@@ -149,11 +149,46 @@ def cpu_baseline(cfg, seconds=10.0, seconds_o0=4.0):
         pass
     return {"value": v, "unit": "scans/s", "cores": 1, "kind": "port",
             "sample": f"1 stream x {done} consecutive synthetic 1081-beam scans, {cfg['map_size']}^2 x "
-                      f"{cfg['levels']} levels, forced map update, oracle/hector_oracle.c -O3 single thread",
+                      f"{cfg['levels']} levels, {'forced map update' if thresholds[0] < 0 else 'thresholds 0.4 m / 0.9 rad'}, "
+                      "oracle/hector_oracle.c -O3 single thread",
             "value_O0": v0, "sample_O0": f"same stream, first {done0} scans, -O0 build", "cpu_model": cpu_model}
 
 
-def pose_check(cfg, S, gpu_poses):
+def _cpu_stream_worker(args):
+    """One CPU process = one stream, as the reference node (one spin thread): scans/s of the oracle."""
+    map_size, levels, seed, n_scans, budget, thresholds = args
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    from slam2d import synth
+
+    S = synth.make_streams(1, n_scans, seed=seed)
+    h = O.HectorOracle(0.05, map_size, (0.5, 0.5), levels, reduce_threads=0)
+    h.set_update_factors(0.4, 0.9)
+    h.set_thresholds(*thresholds)
+    done = 0
+    t0 = time.perf_counter()
+    while done < n_scans and time.perf_counter() - t0 < budget:
+        h.process(S.points[0, done, : S.counts[0, done]])
+        done += 1
+    dt = time.perf_counter() - t0
+    h.close()
+    return done, dt
+
+
+def cpu_baseline_all_cores(cfg, procs, seconds=6.0, thresholds=(-1.0, -1.0)):
+    """`procs` streams on `procs` cores, one process per core, no sharing; aggregate scans/s."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_stream_worker, [(cfg["map_size"], cfg["levels"], 999 + i, 400, seconds, thresholds)
+                                            for i in range(procs)])
+    return {"value": sum(d / t for d, t in res), "unit": "scans/s", "cores": procs,
+            "sample": f"{procs} processes x 1 stream each, <= {seconds:.0f} s of consecutive scans per process, "
+                      "oracle -O3"}
+
+
+def pose_check(cfg, S, gpu_poses, thresholds=(-1.0, -1.0)):
     """Pose error of the benchmarked GPU streams (device pose log, every step incl. warmup) vs the
     CPU oracle in the reference's sequential summation order on the same scans -- the metric's
     'pose RMSE vs ref' -- plus the absolute error against the synthetic ground truth."""
@@ -165,7 +200,7 @@ def pose_check(cfg, S, gpu_poses):
     for s in range(n_streams):
         r = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0)
         r.set_update_factors(0.4, 0.9)
-        r.set_thresholds(-1.0, -1.0)
+        r.set_thresholds(*thresholds)
         for k in range(n_scans):
             rp, _, _ = r.process(S.points[s, k, : S.counts[s, k]])
             e.append(gpu_poses[k, s].astype(np.float64) - rp.astype(np.float64))
@@ -545,6 +580,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--no-copy-probe", action="store_true", help="skip the copy-bandwidth probe")
+    ap.add_argument("--semantics", choices=["forced", "reference"], default="forced",
+                    help="hector: map update every scan (benchmark mode, SURVEY.md 8d) or the node's thresholds "
+                         "0.4 m / 0.9 rad (reference semantics, reported separately)")
+    ap.add_argument("--cpu-cores", type=int, default=16,
+                    help="processes for the all-core CPU baseline (one stream each; the GPU box's CPU share is 16)")
     ap.add_argument("--input", choices=["ranges", "points"], default="ranges",
                     help="hector: raw LaserScan ranges through the on-device ingest (scanCallback, default) or "
                          "pre-converted DataContainer points")
@@ -593,7 +633,9 @@ def main():
 
     fleet = HectorFleet(B, 0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], max_points=1081)
     fleet.set_update_factors(0.4, 0.9)   # hector_slam.cc:144-145
-    fleet.set_thresholds(-1.0, -1.0)     # benchmark mode: update every scan
+    ref_sem = args.semantics == "reference"
+    thr = (0.4, 0.9) if ref_sem else (-1.0, -1.0)
+    fleet.set_thresholds(*thr)           # benchmark mode: update every scan; reference: hector_slam.launch
     hs = torch.cuda.current_stream(dev).cuda_stream
     n_log = min(2, B)
     d_plog = torch.zeros((T, n_log, 3), dtype=torch.float32, device=dev)
@@ -670,18 +712,23 @@ def main():
                 roof["attainable_copy_GBps"] = round(copy_bandwidth(dev), 1)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(cfg)
-        pose = pose_check(cfg, S, d_plog.cpu().numpy())
+            cpu = cpu_baseline(cfg, thresholds=thr)
+            if args.cpu_cores > 1:
+                cpu["all_cores"] = cpu_baseline_all_cores(cfg, args.cpu_cores, thresholds=thr)
+        pose = pose_check(cfg, S, d_plog.cpu().numpy(), thresholds=thr)
         out = {"metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K,
                "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
                "config": {"workload": f"hector_slam match+update, {cfg['map_size']}x{cfg['map_size']} @0.05 m x "
-                                      f"{cfg['levels']} levels, 1081-beam scans, map update every scan",
+                                      f"{cfg['levels']} levels, 1081-beam scans, "
+                                      + ("reference map-update thresholds 0.4 m / 0.9 rad" if ref_sem
+                                         else "map update every scan"),
                           "config": args.config, "streams_per_gpu": B, "global_batch": B * world,
                           "map_size": cfg["map_size"], "levels": cfg["levels"], "beams": 1081,
                           "input": ("LaserScan ranges (on-device ingest in the timed region)" if from_ranges
                                     else "DataContainer points"),
-                          "parallelism": f"replicas x{world}"},
+                          "parallelism": f"replicas x{world}",
+                          "map_updates_per_scan": round(ctr["updates"] / max(B * K, 1), 4)},
                "roofline": roof, "cpu_baseline": cpu, "pose_vs_ref": pose}
         if cpu:
             out["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)

@@ -309,19 +309,30 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
             unsigned rem = num - (unsigned)q * two_da;
             const int la = l.x_major ? 1 : GM_STRIDE, lb = l.x_major ? GM_STRIDE : 1;
             const int A0 = l.x_major ? X0 : Y0, B0 = l.x_major ? Y0 : X0;
-            int li = (l.as + lo - A0) * la + (l.bs + l.sb * q - B0) * lb;
-            const int db_step = l.sb * lb;
-            nfree += hi - lo + 1;
+            const int li = (l.as + lo - A0) * la + (l.bs + l.sb * q - B0) * lb;
+            const int steps = hi - lo + 1;
+            nfree += steps;
             any_tile_marks = true;
-            for (int i = lo; i <= hi; ++i) {
-                atomicAdd(&cnt[li], 1u);              // visits++ (:227-234)
-                li += la;
-                rem += two_db;
-                if (rem >= two_da) {
-                    rem -= two_da;
-                    li += db_step;
-                }
+            // incremental walk with f = 2 da - 1 - rem: the minor axis steps when f - 2 db < 0; byte
+            // offsets into the count array, branch-free, two steps per trip
+            const int tda = (int)two_da, tdb = (int)two_db;
+            const int dab = la * 4, dbb = l.sb * lb * 4;
+            int f = tda - 1 - (int)rem;
+            char *pc = reinterpret_cast<char *>(cnt) + li * 4;
+            int i = 0;
+            for (; i + 1 < steps; i += 2) {
+                atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);  // visits++ (:227-234)
+                int g2 = f - tdb;
+                int m = g2 >> 31;
+                f = g2 + (m & tda);
+                pc += dab + (m & dbb);
+                atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);
+                g2 = f - tdb;
+                m = g2 >> 31;
+                f = g2 + (m & tda);
+                pc += dab + (m & dbb);
             }
+            if (i < steps) atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);
         }
         // tiles without any mark are not written: their stale stamp makes them read as fresh
         if (!__syncthreads_or(any_tile_marks)) continue;

@@ -135,10 +135,21 @@ __device__ __forceinline__ void point_fetch(const float *__restrict__ lvl_words,
 #if S2D_MATCH_ABL == 2
         pf.l[0] = (float)(ix & 7) * 0.01f; pf.l[1] = (float)(iy & 7) * 0.01f; pf.l[2] = 0.0f; pf.l[3] = 0.0f;
 #else
-        pf.l[0] = lvl_words[cell_word(g, ix, iy)];
-        pf.l[1] = lvl_words[cell_word(g, ix + 1, iy)];
-        pf.l[2] = lvl_words[cell_word(g, ix, iy + 1)];
-        pf.l[3] = lvl_words[cell_word(g, ix + 1, iy + 1)];
+        const unsigned ux = (unsigned)ix, uy = (unsigned)iy;  // >= 0 by the bounds check
+        const float *r0 = lvl_words + cell_word(g, (int)ux, (int)uy);
+        const float *r1 = lvl_words + cell_word(g, (int)ux, (int)(uy + 1));
+        if ((ux & (TILE - 1)) != TILE - 1) {
+            // (ix, ix + 1) are adjacent words of one tile row: one 8-byte (4-byte aligned) gather per row
+            float2 a, b;
+            __builtin_memcpy(&a, r0, 8);
+            __builtin_memcpy(&b, r1, 8);
+            pf.l[0] = a.x; pf.l[1] = a.y; pf.l[2] = b.x; pf.l[3] = b.y;
+        } else {
+            pf.l[0] = r0[0];
+            pf.l[1] = lvl_words[cell_word(g, (int)(ux + 1), (int)uy)];
+            pf.l[2] = r1[0];
+            pf.l[3] = lvl_words[cell_word(g, (int)(ux + 1), (int)(uy + 1))];
+        }
 #endif
     }
 }
@@ -253,6 +264,67 @@ __device__ __forceinline__ void gn_step(const float *__restrict__ cells, const L
     }
 }
 
+// gn_step with the thread's points resident in registers (n <= MATCH_THREADS * NP): every gather of
+// the step is issued before the first is consumed -- one memory round trip per Gauss-Newton step.
+// Accumulation order per thread is i = tid, tid + 256, ... as in gn_step.
+template <int NP>
+__device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
+                                            int n, float f, float *est, float *H, float (*red)[MATCH_WAVES][9],
+                                            int parity, int *clamps)
+{
+    const int tid = threadIdx.x;
+    const float cs = sdm_cosf(est[2]);
+    const float sn = sdm_sinf(est[2]);
+    float acc[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
+    PointFetch pf[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+        if (tid + j * MATCH_THREADS < n) point_fetch(cells, g, est[0], est[1], cs, sn, p[j].x * f, p[j].y * f, pf[j]);
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+        if (tid + j * MATCH_THREADS < n) point_accum(pf[j], cs, sn, acc);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc[k] = acc[k] + __shfl_xor(acc[k], off, 64);
+    }
+    const int wave = tid >> 6;
+    if ((tid & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) red[parity][wave][k] = acc[k];
+    }
+    __syncthreads();
+    float s[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        float a0 = red[parity][0][k] + red[parity][2][k];
+        float a1 = red[parity][1][k] + red[parity][3][k];
+        s[k] = a0 + a1;
+    }
+    float b[3] = {s[0], s[1], s[2]};
+    H[0] = s[3]; H[4] = s[4]; H[8] = s[5];
+    H[1] = s[6]; H[2] = s[7]; H[5] = s[8];
+    H[3] = H[1]; H[6] = H[2]; H[7] = H[5];
+    if ((H[0] != 0.0f) && (H[4] != 0.0f)) {
+        float d[3];
+        solve3(H, b, d);
+        if (d[2] > 0.2f) {
+            d[2] = 0.2f;
+            (*clamps)++;
+        } else if (d[2] < -0.2f) {
+            d[2] = -0.2f;
+            (*clamps)++;
+        }
+        est[0] = est[0] + d[0];
+        est[1] = est[1] + d[1];
+        est[2] = est[2] + d[2];
+    }
+}
+
+constexpr int MATCH_REG_PTS = 5;  // points per thread kept in registers: scans of up to 1280 points
+
 __global__ void __launch_bounds__(MATCH_THREADS)
 hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__restrict__ state,
                 const float2 *__restrict__ xy, int xy_stride, const int *__restrict__ counts,
@@ -288,6 +360,13 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     if (mode == MODE_PROCESS || mode == MODE_MATCH_ONLY) {
         // MapRepMultiMap::matchData  H/slam_main/MapRepMultiMap.h:144-167
         float tmp[3] = {hint[0], hint[1], hint[2]};
+        const bool in_regs = n <= MATCH_THREADS * MATCH_REG_PTS;
+        float2 preg[MATCH_REG_PTS];
+#pragma unroll
+        for (int j = 0; j < MATCH_REG_PTS; ++j) {
+            const int i = threadIdx.x + j * MATCH_THREADS;
+            preg[j] = (in_regs && i < n) ? pts[i] : make_float2(0.0f, 0.0f);
+        }
         for (int lvl = geom.levels - 1; lvl >= 0; --lvl) {
             const LevelGeom &g = geom.lv[lvl];
             const int iters = lvl == 0 ? 5 : 3;
@@ -296,7 +375,10 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             float est[3], H[9];
             map_from_world(g, tmp, est);
             for (int it = 0; it <= iters; ++it) {
-                gn_step(lc, g, pts, n, g.pts_scale, est, H, red, parity, &clamps);
+                if (in_regs)
+                    gn_step_reg<MATCH_REG_PTS>(lc, g, preg, n, g.pts_scale, est, H, red, parity, &clamps);
+                else
+                    gn_step(lc, g, pts, n, g.pts_scale, est, H, red, parity, &clamps);
                 parity ^= 1;
             }
             est[2] = normalize_angle(est[2]);

@@ -204,7 +204,7 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     // hs_update_kernel keeps the scan's rays in LDS: beyond 64 KB of dynamic LDS (max_points > ~11k)
     // the binned kernels, whose LDS use is independent of the scan size, take over
     const size_t upd_shmem = sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + (size_t)((c->max_points + 3) & ~3) +
-                                                 4 * (size_t)((c->max_points + 63) / 64));
+                                                 4 * (size_t)fan_groups(c->max_points));
     if (c->update_single && upd_shmem <= 65536) {
         begin_timed(c, 2, s);
         int blocks = 0;

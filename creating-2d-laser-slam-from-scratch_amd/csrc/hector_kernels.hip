@@ -1159,74 +1159,29 @@ __device__ __forceinline__ int upd_off(int row, int tiles_x)
 constexpr int UPD_HIT_WORDS = UPD_TH * (TILE / 32);                  // one hit bit per tile cell
 constexpr int UPD_MARK_WORDS = (UPD_TILE_WORDS + UPD_HIT_WORDS + 3) & ~3;
 
-// ---- lane-balanced raster (S2D_RASTER_CHUNKED) ------------------------------------------------
-// A wave's beams cross a tile with very different free-step counts (none for most beams of a fan
-// far from the origin), so "one lane = one beam" leaves most lanes idle.  Instead each beam's walk
-// clipped to the tile becomes a SEGMENT record (64 per fan group, double-buffered) and is cut into
-// chunks of RC_K steps queued in a per-wave FIFO, drained 64 at a time, one chunk per lane: the lane
-// re-enters the Bresenham walk at the chunk's first step in closed form (one division) and walks
-// on incrementally.  The marks are order-free atomicMin, so any chunk order gives the same tile.
-#ifndef S2D_RASTER_CHUNKED
-#define S2D_RASTER_CHUNKED 0
-#endif
-#ifndef S2D_RC_K
-#define S2D_RC_K 8
-#endif
-constexpr int RC_K = S2D_RC_K;                                 // steps per chunk (power of two)
-constexpr int RC_MAX_STEPS = TILE > UPD_TH ? TILE : UPD_TH;     // free steps of one walk inside one tile
-constexpr int RC_MAX_CH = RC_MAX_STEPS / RC_K;                 // chunks per segment
-static_assert((RC_K & (RC_K - 1)) == 0 && RC_K >= 8 && RC_MAX_CH <= 8, "chunk entry: record (7 bits) | chunk << 7");
-constexpr int RC_RECS = 128;                                   // 2 fan groups x 64 lanes
-constexpr int RC_RING = 128;                                   // FIFO entries (u16): < 64 pending + one pass
-constexpr int RC_WAVE_WORDS = RC_RECS * 4 + RC_RING / 2;
-constexpr int UPD_CHUNK_WORDS = S2D_RASTER_CHUNKED ? (UPD_THREADS / 64) * RC_WAVE_WORDS : 0;
-constexpr int UPD_FIXED_WORDS = UPD_MARK_WORDS + UPD_CHUNK_WORDS;  // + rays + fan-group boxes (per scan size)
-static_assert(UPD_STRIDE >= TILE + 2 && UPD_TH >= 32, "per-lane dummy mark slots live in the row padding");
+constexpr int UPD_FIXED_WORDS = UPD_MARK_WORDS;  // + rays + fan-group boxes (per scan size)
 
 __device__ __forceinline__ int lane_rank(unsigned long long m)  // set lanes below this one
 {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-__device__ __forceinline__ void wave_lds_fence()
+// Fan groups: the 64 beams a wave rasters together.  S2D_FAN_STRIDE 1 (default): 64 consecutive beams
+// (a 16 deg fan at 0.25 deg); 4: beams 256 G + 4 k + w for wave w of super-group G (a 64 deg fan,
+// 1 deg apart), so that near the scan origin the lanes of one LDS atomic address distinct cells --
+// measured slower (0.82 vs 0.78 ms): the wider fans lose more to culling than the conflicts cost.
+#ifndef S2D_FAN_STRIDE
+#define S2D_FAN_STRIDE 1
+#endif
+__device__ __forceinline__ int fan_beam(int b0, int lane)  // b0 = 256 G + 64 w
 {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if S2D_FAN_STRIDE == 4
+    return (b0 & ~255) + 4 * lane + ((b0 >> 6) & 3);
+#else
+    return b0 + lane;
+#endif
 }
-
-// Drain `cnt` (1..64) FIFO entries from position `head`: lane i walks entry head + i.
-__device__ __forceinline__ void rc_round(unsigned *__restrict__ marks, const uint4 *__restrict__ recs,
-                                         const unsigned short *__restrict__ ring, int head, int cnt, int lane,
-                                         int dummy)
-{
-    const unsigned e = ring[(head + lane) & (RC_RING - 1)];
-    const uint4 r = recs[e & (RC_RECS - 1)];
-    const int o = (int)(e >> 7) * RC_K;
-    const int li0 = (int)(r.x & 0xFFFFu);
-    const int das = (int)(signed char)(r.x >> 16);
-    const int dbs = (int)(signed char)(r.x >> 24);
-    const int err0 = (int)(r.y & 0xFFFFu);
-    const int da = (int)(r.z & 0xFFFFu);
-    const int db = (int)(r.z >> 16);
-    const unsigned ev = r.w;
-    int n = (int)(r.y >> 16) - o;
-    n = n < RC_K ? n : RC_K;
-    n = lane < cnt ? n : 0;
-    const unsigned num = (unsigned)err0 + (unsigned)o * (unsigned)db;
-    const int q = (int)udiv_small(num, (unsigned)(da > 0 ? da : 1));
-    // f = da - 1 - error_b: the walk steps the minor axis when f - db < 0 (error_b + db >= da)
-    int f = da - 1 - (int)(num - (unsigned)q * (unsigned)da);
-    int li = li0 + o * das + q * dbs;
-#pragma unroll
-    for (int j = 0; j < RC_K; ++j) {
-        atomicMin(&marks[j < n ? li : dummy], ev);  // bresenhamCellFree (:302-312)
-        const int g = f - db;
-        const int m = g >> 31;  // -1 on a minor step
-        f = g + (m & da);
-        li += das + (m & dbs);
-    }
-}
+__host__ __device__ constexpr int fan_groups(int max_points) { return ((max_points + 255) / 256) * 4; }
 
 // Grid: for level l, upd_parts[l] x count blocks (level-major, then part, then stream); part p of a
 // level draws the tiles t = p, p + parts, ... of the scan's tile box (t row-major over the box).
@@ -1240,12 +1195,6 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     unsigned *rays = smem + UPD_MARK_WORDS;            // max_points packed end cells
     int4 *gbox = reinterpret_cast<int4 *>(rays + ((max_points + 3) & ~3));  // per fan group: x0 y0 x1 y1
     const int lane = threadIdx.x & 63;
-#if S2D_RASTER_CHUNKED
-    unsigned *rc_area = reinterpret_cast<unsigned *>(gbox + (max_points + 63) / 64) + (threadIdx.x >> 6) * RC_WAVE_WORDS;
-    uint4 *rc_recs = reinterpret_cast<uint4 *>(rc_area);
-    unsigned short *rc_ring = reinterpret_cast<unsigned short *>(rc_area + RC_RECS * 4);
-    const int rc_dummy = (lane & 31) * UPD_STRIDE + TILE + (lane >> 5);  // row padding, never applied
-#endif
     __shared__ int s_bbox[4];
 
     // level-major block order: every stream's level 0 (the largest) is dispatched first
@@ -1275,8 +1224,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
     unsigned long long L = 0, R = 0;
     const float2 *pts = xy + (size_t)local * xy_stride;
-    for (int b0 = tid & ~63; b0 < n; b0 += UPD_THREADS) {   // wave-uniform trip count
-        const int b = b0 + lane;
+    for (int b0 = tid & ~63; (b0 & ~255) < n; b0 += UPD_THREADS) {   // wave-uniform trip count
+        const int b = fan_beam(b0, lane);
         unsigned r = RAY_INVALID;
         if (b < n) {
             r = make_ray(g, fr, pts[b]);
@@ -1336,16 +1285,13 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                                                                         : make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
         bool any = false;
-#if S2D_RASTER_CHUNKED
-        int rc_head = 0, rc_tail = 0, rc_par = 0, rc_guard0 = 0, rc_guard1 = 0;  // wave-uniform
-#endif
-        for (int b0 = tid & ~63; b0 < n; b0 += UPD_THREADS) {
+        for (int b0 = tid & ~63; (b0 & ~255) < n; b0 += UPD_THREADS) {
             // wave-uniform fan-group test (scalar)
             const int4 gb = gbox[b0 >> 6];
             const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
             const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
             if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
-            const int b = b0 + lane;
+            const int b = fan_beam(b0, lane);
             const unsigned r = b < n ? rays[b] : RAY_INVALID;
             int scnt = 0;           // free steps of this beam inside the tile
             RayWalk w = {};
@@ -1383,35 +1329,6 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             const int bx = w.b0 + w.sb * q - (w.x_major ? Y0 : X0);
             const int li = ax * la + bx * lb;
             const int da_step = w.sa * la, db_step = w.sb * lb;
-#if S2D_RASTER_CHUNKED
-            const unsigned long long segm = __ballot(scnt > 0);
-            if (segm == 0) continue;
-            // records of this parity are reused: drain every queued chunk of the group that used them
-            const int guard = rc_par ? rc_guard1 : rc_guard0;
-            while (rc_head < guard) {
-                const int c = min(64, rc_tail - rc_head);
-                rc_round(marks, rc_recs, rc_ring, rc_head, c, lane, rc_dummy);
-                rc_head += c;
-            }
-            const int slot = rc_par * 64 + lane;
-            if (scnt > 0)
-                rc_recs[slot] = make_uint4((unsigned)li | ((unsigned)da_step & 0xFFu) << 16 | ((unsigned)db_step & 0xFFu) << 24,
-                                           (unsigned)err | (unsigned)scnt << 16, (unsigned)w.da | (unsigned)w.db << 16, ev);
-            const int nch = (scnt + RC_K - 1) / RC_K;
-            for (int c = 0;; ++c) {  // pass c queues chunk c of every segment that has one
-                const unsigned long long m = __ballot(nch > c);
-                if (m == 0) break;
-                if (nch > c) rc_ring[(rc_tail + lane_rank(m)) & (RC_RING - 1)] = (unsigned short)(slot | (c << 7));
-                rc_tail += __popcll(m);
-                wave_lds_fence();
-                if (rc_tail - rc_head >= 64) {
-                    rc_round(marks, rc_recs, rc_ring, rc_head, 64, lane, rc_dummy);
-                    rc_head += 64;
-                }
-            }
-            if (rc_par) rc_guard1 = rc_tail; else rc_guard0 = rc_tail;
-            rc_par ^= 1;
-#else
 #ifdef S2D_VISITS
             {
                 const unsigned long long am = __ballot(scnt > 0);
@@ -1453,15 +1370,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 pm += dab + (m & dbb);
             }
             if (i < scnt) atomicMin(reinterpret_cast<unsigned *>(pm), ev);
-#endif
         }
-#if S2D_RASTER_CHUNKED
-        while (rc_head < rc_tail) {
-            const int c = min(64, rc_tail - rc_head);
-            rc_round(marks, rc_recs, rc_ring, rc_head, c, lane, rc_dummy);
-            rc_head += c;
-        }
-#endif
         const bool tile_any = __syncthreads_or(any);
 #ifdef S2D_STAMPS
         S2D_STAMP(t_c);

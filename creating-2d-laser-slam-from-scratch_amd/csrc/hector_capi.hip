@@ -80,6 +80,8 @@ struct hs_ctx {
     // part's match / bin kernels (they are latency-bound at low occupancy)
     int nparts = 1;
     int update_single = 1;  // hs_update_kernel (per stream-level, default) or bin + tile kernels
+    int ncu = 256;
+    bool upd_parts_fixed = false;  // SLAM2D_UPD_PARTS given: no batch-size adaptive split
     hipStream_t pstream[MAX_PARTS] = {};
     hipEvent_t ev_start = nullptr, ev_done[MAX_PARTS] = {};
     // scan ingest (hs_set_laser): unit vectors, geometry, the batch's DataContainers
@@ -206,10 +208,24 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     const size_t upd_shmem = sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + (size_t)((c->max_points + 3) & ~3) +
                                                  4 * (size_t)fan_groups(c->max_points));
     if (c->update_single && upd_shmem <= 65536) {
+        FleetGeom gg = c->geom;
+        if (!c->upd_parts_fixed) {
+            // small batches: split each level's tiles over several workgroups so that the grid fills the
+            // CUs (one level-0 workgroup of a 2048^2 scan takes ~0.4 ms alone; a part costs one ray setup)
+            // measured (2048^2 x 3, same box): B = 16: 2 per CU best; B = 64 .. 512: 4 per CU (+8 .. +33 %);
+            // B >= 1024: level 0 in 2 parts (neutral to +1.5 %)
+            const int target = count <= 32 ? 2 : 4;
+            int p0 = (target * c->ncu + count - 1) / count;
+            if (p0 < 2) p0 = 2;
+            for (int l = 0; l < c->levels; ++l) {
+                const int v = p0 >> l;
+                gg.upd_parts[l] = v < 1 ? 1 : (v > 64 ? 64 : v);
+            }
+        }
         begin_timed(c, 2, s);
         int blocks = 0;
-        for (int l = 0; l < c->levels; ++l) blocks += c->geom.upd_parts[l] * count;
-        hipLaunchKernelGGL(hs_update_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
+        for (int l = 0; l < c->levels; ++l) blocks += gg.upd_parts[l] * count;
+        hipLaunchKernelGGL(hs_update_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
                            c->d_state, xy, xy_stride, begin, count, c->max_points);
         end_timed(c, s);
         HCHK(hipGetLastError());
@@ -340,10 +356,12 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         c->nparts = np ? atoi(np) : 1;
         const char *um = getenv("SLAM2D_UPDATE");
         c->update_single = (um && strcmp(um, "binned") == 0) ? 0 : 1;  // measured: single 1.06 ms vs binned 1.30 ms
-        // workgroups per (stream, level) of hs_update_kernel: 1 (splitting a level's tiles over more
-        // workgroups measured slower: each part redoes the ray setup); SLAM2D_UPD_PARTS="p0,p1,..." 
+        // workgroups per (stream, level) of hs_update_kernel: adaptive (launch_part: 1 at >= 512 streams,
+        // where splitting measured neutral to slower), or fixed by SLAM2D_UPD_PARTS="p0,p1,..." 
         for (int l = 0; l < MAX_LEVELS; ++l) c->geom.upd_parts[l] = 1;
+        c->ncu = ncu;
         if (const char *up = getenv("SLAM2D_UPD_PARTS")) {
+            c->upd_parts_fixed = true;
             int l = 0;
             for (const char *q = up; *q && l < MAX_LEVELS; ++l) {
                 const int v = atoi(q);

@@ -154,6 +154,8 @@ __device__ __forceinline__ void point_fetch(const float *__restrict__ lvl_words,
     }
 }
 
+// probs: pf.l already holds the 4 probabilities (neighbourhood cache) instead of log-odds
+template <bool probs = false>
 __device__ __forceinline__ void point_accum(const PointFetch &pf, float cs, float sn, float *acc)
 {
     float v, gx, gy;
@@ -163,10 +165,10 @@ __device__ __forceinline__ void point_accum(const PointFetch &pf, float cs, floa
         gy = 0.0f;
     } else {
         const float fx = pf.fx, fy = pf.fy;
-        float i0 = cell_prob(pf.l[0]);
-        float i1 = cell_prob(pf.l[1]);
-        float i2 = cell_prob(pf.l[2]);
-        float i3 = cell_prob(pf.l[3]);
+        float i0 = probs ? pf.l[0] : cell_prob(pf.l[0]);
+        float i1 = probs ? pf.l[1] : cell_prob(pf.l[1]);
+        float i2 = probs ? pf.l[2] : cell_prob(pf.l[2]);
+        float i3 = probs ? pf.l[3] : cell_prob(pf.l[3]);
         float dx1 = i0 - i1;
         float dx2 = i2 - i3;
         float dy1 = i0 - i2;
@@ -267,10 +269,17 @@ __device__ __forceinline__ void gn_step(const float *__restrict__ cells, const L
 // gn_step with the thread's points resident in registers (n <= MATCH_THREADS * NP): every gather of
 // the step is issued before the first is consumed -- one memory round trip per Gauss-Newton step.
 // Accumulation order per thread is i = tid, tid + 256, ... as in gn_step.
+// Neighbourhood cache: the 4 cell probabilities a point computed last time (GridMapCacheArray's role,
+// GridMapCacheArray.h:48-171), keyed by its cell (iy << 16 | ix), in thread-private LDS slots.  The map
+// is constant during the match, so a point whose cell did not change since the previous Gauss-Newton
+// step (most of them once the pose converges) reuses the values bit for bit and skips the gathers, the
+// 4 exp and the 4 divisions; only waves with a moved point pay a gather round.  Keys reset per level.
+constexpr unsigned NB_NONE = 0xFFFFFFFFu;
+
 template <int NP>
 __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
                                             int n, float f, float *est, float *H, float (*red)[MATCH_WAVES][9],
-                                            int parity, int *clamps)
+                                            int parity, int *clamps, unsigned *nb_key, float4 *nb_val)
 {
     const int tid = threadIdx.x;
     const float cs = sdm_cosf(est[2]);
@@ -279,12 +288,64 @@ __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, con
 #pragma unroll
     for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
     PointFetch pf[NP];
+    unsigned key[NP];
+    bool miss[NP];
 #pragma unroll
-    for (int j = 0; j < NP; ++j)
-        if (tid + j * MATCH_THREADS < n) point_fetch(cells, g, est[0], est[1], cs, sn, p[j].x * f, p[j].y * f, pf[j]);
+    for (int j = 0; j < NP; ++j) {
+        const int slot = tid + j * MATCH_THREADS;
+        miss[j] = false;
+        key[j] = NB_NONE;
+        if (slot < n) {
+            // transform + bounds (point_fetch without the gathers)
+            const float px = p[j].x * f, py = p[j].y * f;
+            const float nsn = -sn;
+            const float x = est[0] + (cs * px + nsn * py);
+            const float y = est[1] + (sn * px + cs * py);
+            pf[j].px = px;
+            pf[j].py = py;
+            pf[j].in = (x >= 0.0f) && (x <= g.lim[0]) && (y >= 0.0f) && (y <= g.lim[1]);  // NaN -> out of map
+            if (pf[j].in) {
+                const int ix = (int)x, iy = (int)y;
+                pf[j].fx = x - (float)ix;
+                pf[j].fy = y - (float)iy;
+                key[j] = ((unsigned)iy << 16) | (unsigned)ix;
+                miss[j] = nb_key[slot] != key[j];
+                if (miss[j]) {
+                    const unsigned ux = (unsigned)ix, uy = (unsigned)iy;
+                    const float *r0 = cells + cell_word(g, (int)ux, (int)uy);
+                    const float *r1 = cells + cell_word(g, (int)ux, (int)(uy + 1));
+                    if ((ux & (TILE - 1)) != TILE - 1) {
+                        float2 a, b;
+                        __builtin_memcpy(&a, r0, 8);
+                        __builtin_memcpy(&b, r1, 8);
+                        pf[j].l[0] = a.x; pf[j].l[1] = a.y; pf[j].l[2] = b.x; pf[j].l[3] = b.y;
+                    } else {
+                        pf[j].l[0] = r0[0];
+                        pf[j].l[1] = cells[cell_word(g, (int)(ux + 1), (int)uy)];
+                        pf[j].l[2] = r1[0];
+                        pf[j].l[3] = cells[cell_word(g, (int)(ux + 1), (int)(uy + 1))];
+                    }
+                }
+            }
+        }
+    }
 #pragma unroll
-    for (int j = 0; j < NP; ++j)
-        if (tid + j * MATCH_THREADS < n) point_accum(pf[j], cs, sn, acc);
+    for (int j = 0; j < NP; ++j) {
+        const int slot = tid + j * MATCH_THREADS;
+        if (slot >= n) continue;
+        if (pf[j].in) {
+            if (miss[j]) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pf[j].l[q] = cell_prob(pf[j].l[q]);
+                nb_val[slot] = make_float4(pf[j].l[0], pf[j].l[1], pf[j].l[2], pf[j].l[3]);
+                nb_key[slot] = key[j];
+            } else {
+                const float4 v = nb_val[slot];
+                pf[j].l[0] = v.x; pf[j].l[1] = v.y; pf[j].l[2] = v.z; pf[j].l[3] = v.w;
+            }
+        }
+        point_accum<true>(pf[j], cs, sn, acc);
+    }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
 #pragma unroll
@@ -333,6 +394,8 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
 {
     static_assert(MATCH_THREADS == 64 * MATCH_WAVES && MATCH_WAVES == 4, "reduction tree assumes 4 waves");
     __shared__ float red[2][MATCH_WAVES][9];
+    __shared__ unsigned nb_key[MATCH_REG_PTS * MATCH_THREADS];
+    __shared__ float4 nb_val[MATCH_REG_PTS * MATCH_THREADS];
     const int local = blockIdx.x;
     const int s = stream_begin + local;
     StreamState &st = state[s];
@@ -374,9 +437,12 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             const float *lc = scells + g.word_offset;
             float est[3], H[9];
             map_from_world(g, tmp, est);
+#pragma unroll
+            for (int j = 0; j < MATCH_REG_PTS; ++j) nb_key[threadIdx.x + j * MATCH_THREADS] = NB_NONE;  // own slots
             for (int it = 0; it <= iters; ++it) {
                 if (in_regs)
-                    gn_step_reg<MATCH_REG_PTS>(lc, g, preg, n, g.pts_scale, est, H, red, parity, &clamps);
+                    gn_step_reg<MATCH_REG_PTS>(lc, g, preg, n, g.pts_scale, est, H, red, parity, &clamps, nb_key,
+                                               nb_val);
                 else
                     gn_step(lc, g, pts, n, g.pts_scale, est, H, red, parity, &clamps);
                 parity ^= 1;

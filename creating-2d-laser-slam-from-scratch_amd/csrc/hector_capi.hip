@@ -82,6 +82,8 @@ struct hs_ctx {
     int update_single = 1;  // hs_update_kernel (per stream-level, default) or bin + tile kernels
     int ncu = 256;
     bool upd_parts_fixed = false;  // SLAM2D_UPD_PARTS given: no batch-size adaptive split
+    UpdList *wl[2] = {nullptr, nullptr};  // lists of updating streams (hector_internal.h)
+    int wl_parity = 0;
     hipStream_t pstream[MAX_PARTS] = {};
     hipEvent_t ev_start = nullptr, ev_done[MAX_PARTS] = {};
     // scan ingest (hs_set_laser): unit vectors, geometry, the batch's DataContainers
@@ -164,6 +166,8 @@ int reset_all(hs_ctx *c)
     HCHK(hipGetLastError());
     std::vector<StreamState> h(c->B, initial_state());
     HCHK(hipMemcpyAsync(c->d_state, h.data(), sizeof(StreamState) * c->B, hipMemcpyHostToDevice, c->stream));
+    for (int i = 0; i < 2; ++i)
+        if (c->wl[i]) HCHK(hipMemsetAsync(c->wl[i], 0, sizeof(int) * 4, c->stream));
     HCHK(hipStreamSynchronize(c->stream));
     return HS_OK;
 }
@@ -197,17 +201,39 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     uint4 *segs = c->d_segs + (size_t)part * c->seg_cap;
     WorkItem *items = c->d_items + (size_t)part * c->item_cap;
     WorkItem *wholes = c->d_wholes + (size_t)part * c->B * c->levels;
+    // the single-kernel update consumes the match kernel's list of updating streams (one part only)
+    const size_t upd_shmem = sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + (size_t)((c->max_points + 3) & ~3) +
+                                                 4 * (size_t)fan_groups(c->max_points));
+    const bool single = c->update_single && upd_shmem <= 65536;
+    const bool use_list = single && c->nparts == 1 && !c->upd_parts_fixed && mode != MODE_MATCH_ONLY;
+    UpdList *wl_cur = use_list ? c->wl[c->wl_parity] : nullptr;
     begin_timed(c, 0, s);
     hipLaunchKernelGGL(hs_match_kernel, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state, xy,
-                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq);
+                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur);
     end_timed(c, s);
     HCHK(hipGetLastError());
     if (mode == MODE_MATCH_ONLY) return HS_OK;
-    // hs_update_kernel keeps the scan's rays in LDS: beyond 64 KB of dynamic LDS (max_points > ~11k)
+    // hs_update_kernel keeps the scan's rays in LDS: beyond 64 KB of dynamic LDS (max_points > ~13k)
     // the binned kernels, whose LDS use is independent of the scan size, take over
-    const size_t upd_shmem = sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + (size_t)((c->max_points + 3) & ~3) +
-                                                 4 * (size_t)fan_groups(c->max_points));
-    if (c->update_single && upd_shmem <= 65536) {
+    if (single && use_list) {
+        // grid for the largest split over U = 1 .. count updating streams; surplus workgroups exit
+        int blocks = 0;
+        for (int U = 1; U <= count; ++U) {
+            int pl[MAX_LEVELS], b = 0;
+            upd_split(U, c->ncu, c->levels, pl);
+            for (int l = 0; l < c->levels; ++l) b += pl[l] * U;
+            blocks = b > blocks ? b : blocks;
+        }
+        UpdList *wl_next = c->wl[c->wl_parity ^ 1];
+        c->wl_parity ^= 1;
+        begin_timed(c, 2, s);
+        hipLaunchKernelGGL(hs_update_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
+                           c->d_state, xy, xy_stride, begin, count, c->max_points, wl_cur, wl_next, c->ncu);
+        end_timed(c, s);
+        HCHK(hipGetLastError());
+        return HS_OK;
+    }
+    if (single) {
         FleetGeom gg = c->geom;
         if (!c->upd_parts_fixed) {
             // small batches: split each level's tiles over several workgroups so that the grid fills the
@@ -226,7 +252,8 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         int blocks = 0;
         for (int l = 0; l < c->levels; ++l) blocks += gg.upd_parts[l] * count;
         hipLaunchKernelGGL(hs_update_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
-                           c->d_state, xy, xy_stride, begin, count, c->max_points);
+                           c->d_state, xy, xy_stride, begin, count, c->max_points, (const UpdList *)nullptr,
+                           (UpdList *)nullptr, c->ncu);
         end_timed(c, s);
         HCHK(hipGetLastError());
         return HS_OK;
@@ -394,7 +421,9 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         (e = hipMalloc(&c->d_segs, sizeof(uint4) * (size_t)c->seg_cap * c->nparts)) != hipSuccess ||
         (e = hipMalloc(&c->d_items, sizeof(WorkItem) * (size_t)c->item_cap * c->nparts)) != hipSuccess ||
         (e = hipMalloc(&c->d_wholes, sizeof(WorkItem) * (size_t)num_streams * levels * c->nparts)) != hipSuccess ||
-        (e = hipMalloc(&c->d_wq, sizeof(WorkQueue) * c->nparts)) != hipSuccess) {
+        (e = hipMalloc(&c->d_wq, sizeof(WorkQueue) * c->nparts)) != hipSuccess ||
+        (e = hipMalloc(&c->wl[0], sizeof(int) * (4 + (size_t)num_streams))) != hipSuccess ||
+        (e = hipMalloc(&c->wl[1], sizeof(int) * (4 + (size_t)num_streams))) != hipSuccess) {
         hs_destroy(c);
         return fail(HS_ENOMEM, "hipMalloc", e);
     }
@@ -437,6 +466,8 @@ int hs_destroy(hs_ctx *c)
     hipFree(c->d_items);
     hipFree(c->d_wholes);
     hipFree(c->d_wq);
+    hipFree(c->wl[0]);
+    hipFree(c->wl[1]);
     hipFree(c->d_cs);
     hipFree(c->d_ixy);
     hipFree(c->d_in);

@@ -103,6 +103,29 @@ struct WorkQueue {
     unsigned item_cap, seg_cap, pad_[2];
 };
 
+// Streams whose map is updated this step, appended by hs_match_kernel (order-free: the per-stream work
+// is independent), consumed by hs_update_kernel.  Two lists alternate: the update kernel reads one and
+// clears the other, which the next step's match kernel fills.
+struct UpdList {
+    int count;
+    int pad_[3];
+    int stream[1];  // [B] local stream indices
+};
+
+// Workgroups per (stream, level) of hs_update_kernel for U updating streams on ncu CUs: about 4 level-0
+// workgroups per CU for small batches (2 for U <= 32), at least 2 for level 0, halved per level
+// (measured).
+inline __host__ __device__ void upd_split(int U, int ncu, int levels, int *parts)
+{
+    const int target = U <= 32 ? 2 : 4;
+    int p0 = U > 0 ? (target * ncu + U - 1) / U : 1;
+    if (p0 < 2) p0 = 2;
+    for (int l = 0; l < levels; ++l) {
+        const int v = p0 >> l;
+        parts[l] = v < 1 ? 1 : (v > 64 ? 64 : v);
+    }
+}
+
 // Optional device pose log: the match kernel appends every step's pose of streams [0, streams).
 struct PoseLog {
     float *buf;    // [capacity][streams][3]

@@ -390,7 +390,8 @@ __global__ void __launch_bounds__(MATCH_THREADS)
 hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__restrict__ state,
                 const float2 *__restrict__ xy, int xy_stride, const int *__restrict__ counts,
                 const float2 *__restrict__ origo, const float *__restrict__ hints, int stream_begin, int mode,
-                float *__restrict__ out_pose, float *__restrict__ out_cov, PoseLog plog, WorkQueue *__restrict__ wq)
+                float *__restrict__ out_pose, float *__restrict__ out_cov, PoseLog plog, WorkQueue *__restrict__ wq,
+                UpdList *__restrict__ wl)
 {
     static_assert(MATCH_THREADS == 64 * MATCH_WAVES && MATCH_WAVES == 4, "reduction tree assumes 4 waves");
     __shared__ float red[2][MATCH_WAVES][9];
@@ -514,6 +515,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
         st.map_updates += 1;                 // GridMapBase::setUpdated (GridMapBase.h:333)
         st.step_cells = 0;
         st.tot_updates += 1;
+        if (wl) wl->stream[atomicAdd(&wl->count, 1)] = local;
     }
 }
 
@@ -1253,7 +1255,8 @@ __host__ __device__ constexpr int fan_groups(int max_points) { return ((max_poin
 // level draws the tiles t = p, p + parts, ... of the scan's tile box (t row-major over the box).
 __global__ void __launch_bounds__(UPD_THREADS, S2D_UPD_MINB)
 hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restrict__ state,
-                 const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points)
+                 const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points,
+                 const UpdList *__restrict__ wl, UpdList *__restrict__ wl_next, int ncu)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned smem[];
     unsigned *marks = smem;                            // UPD_TILE_WORDS event words
@@ -1264,11 +1267,25 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     __shared__ int s_bbox[4];
 
     // level-major block order: every stream's level 0 (the largest) is dispatched first
-    int lvl = 0, idx = (int)blockIdx.x;
-    while (lvl + 1 < geom.levels && idx >= geom.upd_parts[lvl] * count) idx -= geom.upd_parts[lvl++] * count;
-    const int parts = geom.upd_parts[lvl];
-    const int part = idx / count;
-    const int local = idx - part * count;
+    int lvl = 0, idx = (int)blockIdx.x, parts, part, local;
+    if (wl) {
+        // the U streams the match kernel listed, split by U (not by the batch size): with the node's
+        // map-update gate only a fraction of the streams update, and they get the whole grid
+        const int U = wl->count;
+        if (blockIdx.x == 0 && threadIdx.x == 0) wl_next->count = 0;
+        int pl[MAX_LEVELS];
+        upd_split(U, ncu, geom.levels, pl);
+        while (lvl + 1 < geom.levels && idx >= pl[lvl] * U) idx -= pl[lvl++] * U;
+        if (idx >= pl[lvl] * U) return;  // the grid is sized for the largest split (host)
+        parts = pl[lvl];
+        part = idx / U;
+        local = wl->stream[idx - part * U];
+    } else {
+        while (lvl + 1 < geom.levels && idx >= geom.upd_parts[lvl] * count) idx -= geom.upd_parts[lvl++] * count;
+        parts = geom.upd_parts[lvl];
+        part = idx / count;
+        local = idx - part * count;
+    }
     const int s = stream_begin + local;
     const StreamState &st = state[s];
     if (!st.do_update) return;

@@ -354,3 +354,62 @@ def test_nan_pose_is_out_of_map(gpu):
         assert (fleet.get_map(0, lvl)["upd"] >= 0).sum() == 0
     gp, _ = fleet.match(0, pts, np.array([np.nan] * 3, np.float32))
     assert np.isnan(gp).all()
+
+
+# ----------------------------------------------------------------------------- scan-size edge cases
+@pytest.mark.parametrize("n_beams,levels,size", [(2400, 3, 1024), (16000, 2, 512)])
+def test_dense_scans_bitexact(gpu, n_beams, levels, size):
+    """Scans larger than the match kernel's register-resident points (> 1280: the strided loop) and,
+    at 16000 beams, larger than the single-kernel update's LDS budget (the binned update takes
+    over): poses, gate and maps bit-exact vs the oracle."""
+    S = synth.make_streams(1, 6, seed=4711, n_beams=n_beams)
+    fleet = HectorFleet(1, 0.05, size, (0.5, 0.5), levels, max_points=n_beams)
+    ora = O.HectorOracle(0.05, size, (0.5, 0.5), levels, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(-1.0, -1.0)
+    assert S.counts.max() > 1280
+    for k in range(6):
+        pts = S.points[0, k, : S.counts[0, k]]
+        gp, _, gd = fleet.update(0, pts)
+        op, _, od = ora.process(pts)
+        assert gd == od
+        np.testing.assert_array_equal(_bits(gp), _bits(op), err_msg=f"scan {k}")
+    for lvl in range(levels):
+        m = fleet.get_map(0, lvl)
+        ol, ou = ora.level(lvl)
+        np.testing.assert_array_equal(m["upd"], ou)
+        np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))
+
+
+@pytest.mark.parametrize("B", [40, 600])
+def test_batch_sizes_across_split_rules(gpu, B):
+    """The update's batch-adaptive tile split (B = 40: 25 level-0 workgroups per stream; B = 600: 2) vs
+    the oracle on a sample of streams, 3 steps, 3 levels: poses and maps bit-exact."""
+    import torch
+
+    T = 3
+    S = synth.make_streams(B, T, seed=99)
+    fleet = HectorFleet(B, 0.05, 1024, (0.5, 0.5), 3, max_points=1081)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(-1.0, -1.0)
+    check = [0, 1, B // 2, B - 1]
+    oras = {s: O.HectorOracle(0.05, 1024, (0.5, 0.5), 3, reduce_threads=T_RED) for s in check}
+    for o in oras.values():
+        o.set_update_factors(0.4, 0.9)
+        o.set_thresholds(-1.0, -1.0)
+    for t in range(T):
+        d_xy = _torch_dev(S.points[:, t])
+        d_n = _torch_dev(S.counts[:, t].astype(np.int32))
+        fleet.step_device(d_xy.data_ptr(), 1081, d_n.data_ptr())
+        torch.cuda.synchronize()
+        gp = fleet.poses()[0]
+        for s in check:
+            op, _, _ = oras[s].process(S.points[s, t, : S.counts[s, t]])
+            np.testing.assert_array_equal(_bits(gp[s]), _bits(op), err_msg=f"t={t} s={s}")
+    for s in check:
+        for lvl in range(3):
+            m = fleet.get_map(s, lvl)
+            ol, ou = oras[s].level(lvl)
+            np.testing.assert_array_equal(m["upd"], ou)
+            np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))

@@ -279,6 +279,26 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
             const double wy = (s * spx[k] + c * spy[k]) + x_old[1];
             int from, to;
             pl_interval(p, wx, wy, n, min_theta, max_theta, from, to);
+            {
+                // Prune the interval to the reference points that can pass the maxd2 test: a point at
+                // polar angle theta_j is at least |w| sin|theta_w - theta_j| from w, so beyond
+                // asin(1.01 maxd / |w|) (+3 cells for the interval's cell mapping) its distance exceeds
+                // maxd by 1 % -- the exhaustive scan would skip it.  The candidates kept are visited in
+                // the same order, so the result is the exhaustive search's, bit for bit.
+                const double norm = sqrt(wx * wx + wy * wy);
+                const double lim = 1.01 * p.max_correspondence_dist;
+                if (norm > 2.0 * lim && angle_inc > 0.0) {
+                    const double sn_ = lim / norm;
+                    const double dth = sdm_atan(sn_ / sqrt(1.0 - sn_ * sn_));
+                    double th = sdm_atan2(wy, wx);
+                    if (th < min_theta) th += 2.0 * SDM_PI;
+                    if (th > max_theta) th -= 2.0 * SDM_PI;
+                    const int cw = (int)((th - min_theta) / angle_inc);
+                    const int m = (int)ceil(dth / angle_inc) + 3;
+                    from = from > cw - m ? from : cw - m;
+                    to = to < cw + m ? to : cw + m;
+                }
+            }
             int b1 = -1;
             double best = 0.0;
             for (int j = from; j <= to; ++j) {

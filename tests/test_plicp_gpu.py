@@ -80,3 +80,21 @@ def test_batch_device(gpu):
         r = PlResult.from_buffer_copy(raw[b].tobytes())
         g = dict(x=np.array(r.x[:]), valid=bool(r.valid), iterations=r.iterations, nvalid=r.nvalid, error=r.error)
         _same(g, O.plicp(pairs[b][0], pairs[b][1], amin, inc, reduce_threads=256))
+
+
+@pytest.mark.parametrize("n_beams,scale", [(1440, 1.0), (1081, 0.2), (1440, 0.12)])
+def test_full_circle_and_near_scans(gpu, n_beams, scale):
+    """The correspondence search prunes the polar interval by the angular distance bound (kept
+    candidates visited in the same order): a 360-degree scan (1440 beams from -135 deg, wrapping past
+    pi) and scaled-down worlds whose points sit around the pruning threshold (2.02 m) -- bit-exact vs
+    the oracle's exhaustive interval scan."""
+    rng = np.random.default_rng(77 + n_beams)
+    ang0 = float(synth.ANGLE_MIN)
+    inc = float(np.float64(synth.ANGLE_INC))
+    gt = synth.trajectory(5, 1.1)
+    R = synth.cast_ranges(gt, synth.world_segments(), n_beams) * scale
+    R = R + rng.normal(0, 0.01 * scale, R.shape)
+    R = laser_scan_to_readings(R, 0.05, 29.9)
+    pl = PLICP(1, n_beams)
+    for k in range(4):
+        _same(pl.icp(R[k], R[k + 1], ang0, inc), O.plicp(R[k], R[k + 1], ang0, inc, reduce_threads=256))

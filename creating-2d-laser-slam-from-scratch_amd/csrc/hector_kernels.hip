@@ -1229,6 +1229,17 @@ constexpr int UPD_MARK_WORDS = (UPD_TILE_WORDS + UPD_HIT_WORDS + 3) & ~3;
 
 constexpr int UPD_FIXED_WORDS = UPD_MARK_WORDS;  // + rays + fan-group boxes (per scan size)
 
+// the free mark of one raster step: blind LDS atomicMin of the event code (S2D_DIAG_PLAIN: a plain
+// store -- wrong results, a diagnostic build that prices the atomic)
+__device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev)
+{
+#ifdef S2D_DIAG_PLAIN
+    *reinterpret_cast<volatile unsigned *>(p) = ev;
+#else
+    atomicMin(p, ev);
+#endif
+}
+
 __device__ __forceinline__ int lane_rank(unsigned long long m)  // set lanes below this one
 {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -1441,18 +1452,18 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             char *pm = reinterpret_cast<char *>(marks) + li * 4;
             int i = 0;
             for (; i + 1 < scnt; i += 2) {
-                atomicMin(reinterpret_cast<unsigned *>(pm), ev);  // bresenhamCellFree (:302-312)
+                upd_mark(reinterpret_cast<unsigned *>(pm), ev);  // bresenhamCellFree (:302-312)
                 int g2 = f - db_;
                 int m = g2 >> 31;
                 f = g2 + (m & da_);
                 pm += dab + (m & dbb);
-                atomicMin(reinterpret_cast<unsigned *>(pm), ev);
+                upd_mark(reinterpret_cast<unsigned *>(pm), ev);
                 g2 = f - db_;
                 m = g2 >> 31;
                 f = g2 + (m & da_);
                 pm += dab + (m & dbb);
             }
-            if (i < scnt) atomicMin(reinterpret_cast<unsigned *>(pm), ev);
+            if (i < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
         }
         const bool tile_any = __syncthreads_or(any);
 #ifdef S2D_STAMPS

@@ -1472,6 +1472,10 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         t_b = t_c;
 #endif
         if (!tile_any) continue;
+#ifdef S2D_DIAG_NOAPPLY
+        __syncthreads();
+        continue;  // diagnostic build only: the tile's apply phase skipped
+#endif
         // apply: thread owns quads q = tid + j * 256 (16 quads per 64-cell row): 16-B LDS reads of the
         // event words, 16-B global loads / stores of both planes for every quad holding a mark.  Cells
         // outside the map (padding of edge tiles) never carry marks and are rewritten unchanged.

@@ -117,6 +117,9 @@ __device__ __forceinline__ bool pl_gpc_solve(const double *m, double *x)
     double lo = -lmin, hi = -lmin + hn;
     for (int it = 0; it < 200; ++it) {
         const double l = 0.5 * (lo + hi);
+        // converged: the midpoint is an endpoint, so every further step would assign lo or hi its own
+        // value -- stopping here leaves the oracle's 200-step result unchanged, bit for bit
+        if (l == lo || l == hi) break;
         const double a = s00 + l, d = s11 + l;
         const double det = a * d - s01 * s01;
         const double r0 = (d * h0 - s01 * h1) / det, r1 = (a * h1 - s01 * h0) / det;

@@ -200,6 +200,8 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
     __shared__ unsigned long long s_pref[2];
     __shared__ int s_rank[2];
     __shared__ unsigned s_hash[PL_MAX_IT];
+    __shared__ double s_x[3];
+    __shared__ int s_ok;
 
     const int pair = blockIdx.x;
     const int tid = threadIdx.x;
@@ -361,18 +363,46 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                 if (m1) atomicAdd(&hist[256 + d], 1u);
             }
             __syncthreads();
-            if (tid == 0 || tid == 64) {
-                const int h = tid == 0 ? 0 : 1;
-                int r = h == 0 ? rank0 : rank1;
-                unsigned cum = 0;
-                int b = 0;
-                for (; b < 255; ++b) {
-                    const unsigned c2 = hist[256 * h + b];
-                    if (cum + c2 > (unsigned)r) break;
-                    cum += c2;
+            if (tid < 128) {
+                // wave h selects in histogram h: the first bin b < 255 whose inclusive count exceeds
+                // the rank (else 255), and the count before it -- a wave prefix scan over 4 bins per lane
+                // (the same b and count as a sequential walk over the bins)
+                const int h = tid >> 6, lane = tid & 63;
+                const unsigned r = (unsigned)(h == 0 ? rank0 : rank1);
+                const unsigned *hh = hist + 256 * h;
+                unsigned c[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) c[j] = hh[4 * lane + j];
+                const unsigned sum4 = (c[0] + c[1]) + (c[2] + c[3]);
+                unsigned incl = sum4;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const unsigned t = __shfl_up(incl, off, 64);
+                    if (lane >= off) incl += t;
                 }
-                s_pref[h] = (h == 0 ? pref0 : pref1) | ((unsigned long long)b << shift);
-                s_rank[h] = r - (int)cum;
+                unsigned cum = incl - sum4;
+                int jf = -1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (jf >= 0) continue;
+                    if (4 * lane + j < 255 && cum + c[j] > r) jf = j;
+                    else cum += c[j];
+                }
+                const unsigned long long m = __ballot(jf >= 0);
+                int b;
+                unsigned cb;
+                if (m) {
+                    const int src = __ffsll((long long)m) - 1;
+                    b = 4 * src + __shfl(jf, src, 64);
+                    cb = __shfl(cum, src, 64);
+                } else {
+                    b = 255;
+                    cb = __shfl(incl - c[3], 63, 64);  // bins 0 .. 254
+                }
+                if (lane == 0) {
+                    s_pref[h] = (h == 0 ? pref0 : pref1) | ((unsigned long long)b << shift);
+                    s_rank[h] = (int)(r - cb);
+                }
             }
             __syncthreads();
             pref0 = s_pref[0];
@@ -447,7 +477,23 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
         __syncthreads();
         const unsigned hash = ((unsigned)sred[0] + (unsigned)sred[1] + (unsigned)sred[2] + (unsigned)sred[3]) & 0x7FFFFFFFu;
         __syncthreads();
-        if (!pl_gpc_solve(m, x_new)) {
+        // the constrained solve once per pair (wave 0), broadcast: on failure x_new keeps what
+        // pl_gpc_solve left in it, as in the all-threads version
+        if (tid < 64) {
+            double xs[3] = {x_new[0], x_new[1], x_new[2]};
+            const bool okk = pl_gpc_solve(m, xs);
+            if (tid == 0) {
+                s_x[0] = xs[0];
+                s_x[1] = xs[1];
+                s_x[2] = xs[2];
+                s_ok = okk ? 1 : 0;
+            }
+        }
+        __syncthreads();
+        x_new[0] = s_x[0];
+        x_new[1] = s_x[1];
+        x_new[2] = s_x[2];
+        if (!s_ok) {
             all_ok = false;
             break;
         }

@@ -233,18 +233,27 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
             }
         }
     }
-    // next valid neighbours of every reference ray (wave 0 scans serially in both directions)
-    if (tid == 0) {
-        int last = -1;
-        for (int i = 0; i < n; ++i) {
-            rdn[i] = (int16_t)last;
-            if (rr[i] > 0.0) last = i;
-        }
-    } else if (tid == 64) {
-        int last = -1;
-        for (int i = n - 1; i >= 0; --i) {
-            rup[i] = (int16_t)last;
-            if (rr[i] > 0.0) last = i;
+    // next valid neighbours of every reference ray: wave 0 the nearest valid ray below, wave 1 above,
+    // 64 rays per step from the validity ballot and a carry across the steps
+    if (tid < 128) {
+        const int lane = tid & 63;
+        const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes < lane
+        const unsigned long long above = lane < 63 ? (~0ull << (lane + 1)) : 0ull;  // lanes > lane
+        int carry = -1;
+        const int nch = (n + 63) / 64;
+        for (int c = 0; c < nch; ++c) {
+            const int ch = tid < 64 ? c : nch - 1 - c;
+            const int i = ch * 64 + lane;
+            const unsigned long long m = __ballot(i < n && rr[i] > 0.0);
+            if (tid < 64) {
+                const unsigned long long mb = m & below;
+                if (i < n) rdn[i] = (int16_t)(mb ? ch * 64 + 63 - __clzll((long long)mb) : carry);
+                if (m) carry = ch * 64 + 63 - __clzll((long long)m);
+            } else {
+                const unsigned long long ma = m & above;
+                if (i < n) rup[i] = (int16_t)(ma ? ch * 64 + __ffsll((long long)ma) - 1 : carry);
+                if (m) carry = ch * 64 + __ffsll((long long)m) - 1;
+            }
         }
     }
     __syncthreads();

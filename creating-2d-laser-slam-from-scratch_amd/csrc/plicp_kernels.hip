@@ -196,9 +196,9 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
     int16_t *rdn = rup + n;                                                         // next valid below [n]
     __shared__ double red[4][16];
     __shared__ int sred[4];
-    __shared__ unsigned hist[512];
-    __shared__ unsigned long long s_pref[2];
-    __shared__ int s_rank[2];
+    __shared__ unsigned hist[2 * 512];
+    __shared__ unsigned long long s_pref[2], s_key[2];
+    __shared__ int s_rank[2], s_one[2];
     __shared__ unsigned s_hash[PL_MAX_IT];
     __shared__ double s_x[3];
     __shared__ int s_ok;
@@ -367,6 +367,7 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
             const double2 q1 = rpt[b1], q2 = rpt[b2];
             e[k] = pl_dist_to_segment(q1.x, q1.y, q2.x, q2.y, wx, wy);
         }
+        for (int b = tid; b < 512; b += PL_THREADS) hist[b] = 0;   // first radix pass's buffer
         ncorr = pl_block_sum_int(ncorr, sred);
         if (ncorr < 0.05 * n) {
             all_ok = false;
@@ -378,11 +379,16 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
         order = order < 0 ? 0 : (order > kk - 1 ? kk - 1 : order);
         int order2 = (int)floor(kk * p.outliers_adaptive_order);
         order2 = order2 < 0 ? 0 : (order2 > kk - 1 ? kk - 1 : order2);
+        // Two histogram buffers: a pass accumulates into one and clears the other for the next pass.
+        // A statistic is settled early once its selected bin holds a single key: that key is the
+        // answer, fetched from its owner (the same value the remaining passes would spell out).
         unsigned long long pref0 = 0, pref1 = 0;
         int rank0 = order, rank1 = order2;
-        for (int shift = 56; shift >= 0; shift -= 8) {
-            for (int b = tid; b < 512; b += PL_THREADS) hist[b] = 0;
-            __syncthreads();
+        bool done0 = false, done1 = false;
+        int cur = 0;
+        for (int shift = 56; shift >= 0 && !(done0 && done1); shift -= 8, cur ^= 1) {
+            unsigned *hc = hist + 512 * cur;
+            for (int b = tid; b < 512; b += PL_THREADS) hist[512 * (cur ^ 1) + b] = 0;
 #pragma unroll
             for (int k = 0; k < PL_RPT; ++k) {
                 if (!ok[k]) continue;
@@ -390,17 +396,17 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                 const unsigned d = (unsigned)(key >> shift) & 255u;
                 const bool m0 = shift == 56 || (key >> (shift + 8)) == (pref0 >> (shift + 8));
                 const bool m1 = shift == 56 || (key >> (shift + 8)) == (pref1 >> (shift + 8));
-                if (m0) atomicAdd(&hist[d], 1u);
-                if (m1) atomicAdd(&hist[256 + d], 1u);
+                if (m0 && !done0) atomicAdd(&hc[d], 1u);
+                if (m1 && !done1) atomicAdd(&hc[256 + d], 1u);
             }
             __syncthreads();
-            if (tid < 128) {
+            if (tid < 128 && !(tid < 64 ? done0 : done1)) {
                 // wave h selects in histogram h: the first bin b < 255 whose inclusive count exceeds
                 // the rank (else 255), and the count before it -- a wave prefix scan over 4 bins per lane
                 // (the same b and count as a sequential walk over the bins)
                 const int h = tid >> 6, lane = tid & 63;
                 const unsigned r = (unsigned)(h == 0 ? rank0 : rank1);
-                const unsigned *hh = hist + 256 * h;
+                const unsigned *hh = hc + 256 * h;
                 unsigned c[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) c[j] = hh[4 * lane + j];
@@ -433,14 +439,37 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                 if (lane == 0) {
                     s_pref[h] = (h == 0 ? pref0 : pref1) | ((unsigned long long)b << shift);
                     s_rank[h] = (int)(r - cb);
+                    s_one[h] = hh[b] == 1u;
                 }
             }
             __syncthreads();
-            pref0 = s_pref[0];
-            pref1 = s_pref[1];
-            rank0 = s_rank[0];
-            rank1 = s_rank[1];
-            __syncthreads();
+            const bool one0 = !done0 && s_one[0], one1 = !done1 && s_one[1];
+            if (!done0) {
+                pref0 = s_pref[0];
+                rank0 = s_rank[0];
+            }
+            if (!done1) {
+                pref1 = s_pref[1];
+                rank1 = s_rank[1];
+            }
+            if (one0 || one1) {
+#pragma unroll
+                for (int k = 0; k < PL_RPT; ++k) {
+                    if (!ok[k]) continue;
+                    const unsigned long long key = (unsigned long long)__double_as_longlong(e[k]);
+                    if (one0 && (key >> shift) == (pref0 >> shift)) s_key[0] = key;
+                    if (one1 && (key >> shift) == (pref1 >> shift)) s_key[1] = key;
+                }
+                __syncthreads();
+                if (one0) {
+                    pref0 = s_key[0];
+                    done0 = true;
+                }
+                if (one1) {
+                    pref1 = s_key[1];
+                    done1 = true;
+                }
+            }
         }
         const double lim1 = __longlong_as_double((long long)pref0);
         const double lim2 = p.outliers_adaptive_mult * __longlong_as_double((long long)pref1);

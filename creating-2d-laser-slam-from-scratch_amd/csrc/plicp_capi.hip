@@ -130,8 +130,13 @@ static int pl_launch(pl_ctx *c, int count, int n, double angle_min, double angle
         }
         PCHK(hipEventRecord(ev.first, s));
     }
-    hipLaunchKernelGGL(pl_icp_kernel, dim3(count), dim3(PL_THREADS), pl_shmem(n), s, c->params, n, angle_min, angle_inc,
-                       d_ref, d_sens, d_guess, d_res);
+    {
+        const int rpt = (n + PL_THREADS - 1) / PL_THREADS;
+        auto kern = rpt <= 2 ? pl_icp_kernel<2> : rpt <= 4 ? pl_icp_kernel<4> : rpt <= 5 ? pl_icp_kernel<5>
+                  : rpt <= 6 ? pl_icp_kernel<6> : pl_icp_kernel<PL_RPT_MAX>;
+        hipLaunchKernelGGL(kern, dim3(count), dim3(PL_THREADS), pl_shmem(n), s, c->params, n, angle_min, angle_inc,
+                           d_ref, d_sens, d_guess, d_res);
+    }
     PCHK(hipGetLastError());
     if (c->timing) {
         PCHK(hipEventRecord(ev.second, s));

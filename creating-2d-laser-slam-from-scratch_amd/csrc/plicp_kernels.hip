@@ -24,8 +24,8 @@
 namespace s2d {
 
 constexpr int PL_THREADS = 256;
-constexpr int PL_RPT = 8;                       // rays per thread: max_rays <= 2048
-constexpr int PL_MAX_RAYS = PL_THREADS * PL_RPT;
+constexpr int PL_RPT_MAX = 8;                   // rays per thread: max_rays <= 2048
+constexpr int PL_MAX_RAYS = PL_THREADS * PL_RPT_MAX;
 constexpr int PL_MAX_IT = 64;
 
 __device__ __forceinline__ double pl_dist_to_segment(double ax, double ay, double bx, double by, double x, double y)
@@ -93,7 +93,7 @@ __device__ __forceinline__ void pl_terms(double px, double py, double qx, double
 }
 
 // constrained point-to-line solve (the role of CSM's gpc_solve); false if degenerate
-__device__ __forceinline__ bool pl_gpc_solve(const double *m, double *x)
+__device__ __attribute__((noinline)) bool pl_gpc_solve(const double *m, double *x)
 {
     const double m00 = m[0], m01 = m[1], m02 = m[2], m03 = m[3], m11 = m[4], m12 = m[5], m13 = m[6];
     const double m22 = m[7], m23 = m[8], m33 = m[9];
@@ -185,7 +185,15 @@ __device__ __forceinline__ int pl_block_sum_int(int v, int *sred)
     return r;
 }
 
-__global__ void __launch_bounds__(PL_THREADS)
+// register budget knob for occupancy experiments (waves per SIMD the compiler must fit)
+#ifndef PL_WAVES_PER_EU
+#define PL_WAVES_PER_EU 1
+#endif
+// PL_RPT = rays per thread, instantiated per scan length (the host picks the smallest that covers n):
+// thread t owns rays t + 256 k, k < PL_RPT, so the rays and their summation order are the same for
+// every instantiation -- only the register arrays shrink.
+template <int PL_RPT>
+__global__ void __launch_bounds__(PL_THREADS) __attribute__((amdgpu_waves_per_eu(PL_WAVES_PER_EU)))
 pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const double *__restrict__ ref_r,
               const double *__restrict__ sens_r, const double *__restrict__ first_guess, pl_result *__restrict__ out)
 {

@@ -185,9 +185,10 @@ __device__ __forceinline__ int pl_block_sum_int(int v, int *sred)
     return r;
 }
 
-// register budget knob for occupancy experiments (waves per SIMD the compiler must fit)
+// register budget: 4 waves per SIMD (4 pairs per CU).  The kernel wants ~170 VGPRs; capping it at 128
+// spills a few cold values to scratch but doubles the resident pairs (A/B: 0.92 M -> 1.21 M pairs/s)
 #ifndef PL_WAVES_PER_EU
-#define PL_WAVES_PER_EU 1
+#define PL_WAVES_PER_EU 4
 #endif
 // PL_RPT = rays per thread, instantiated per scan length (the host picks the smallest that covers n):
 // thread t owns rays t + 256 k, k < PL_RPT, so the rays and their summation order are the same for
@@ -376,6 +377,10 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
             e[k] = pl_dist_to_segment(q1.x, q1.y, q2.x, q2.y, wx, wy);
         }
         for (int b = tid; b < 512; b += PL_THREADS) hist[b] = 0;   // first radix pass's buffer
+        if (p.outliers_remove_doubles) {
+            const unsigned long long init = (unsigned long long)__double_as_longlong(1000000.0);
+            for (int j = tid; j < n; j += PL_THREADS) best_j[j] = init;
+        }
         ncorr = pl_block_sum_int(ncorr, sred);
         if (ncorr < 0.05 * n) {
             all_ok = false;
@@ -482,25 +487,22 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
         const double lim1 = __longlong_as_double((long long)pref0);
         const double lim2 = p.outliers_adaptive_mult * __longlong_as_double((long long)pref1);
         const double limit = lim1 < lim2 ? lim1 : lim2;
-        double err_sum[1] = {0.0};
-        int nv = 0;
+        // the error sum and the kept count in one reduction (the count rides as an exact small double)
+        double err_sum[2] = {0.0, 0.0};
 #pragma unroll
         for (int k = 0; k < PL_RPT; ++k) {
             if (!ok[k]) continue;
             if (e[k] > limit) ok[k] = false;
             else {
-                ++nv;
+                err_sum[1] += 1.0;
                 err_sum[0] = err_sum[0] + e[k];
             }
         }
-        nvalid = pl_block_sum_int(nv, sred);
-        pl_block_sum<1>(err_sum, red);
+        pl_block_sum<2>(err_sum, red);
         total_error = err_sum[0];
-        // ---- kill_outliers_double
+        nvalid = (int)err_sum[1];
+        // ---- kill_outliers_double (best_j was reset at the top of the iteration)
         if (p.outliers_remove_doubles) {
-            const unsigned long long init = (unsigned long long)__double_as_longlong(1000000.0);
-            for (int j = tid; j < n; j += PL_THREADS) best_j[j] = init;
-            __syncthreads();
 #pragma unroll
             for (int k = 0; k < PL_RPT; ++k)
                 if (ok[k]) atomicMin(&best_j[j1[k]], (unsigned long long)__double_as_longlong(d2[k]));
@@ -538,19 +540,30 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
 #pragma unroll
             for (int q = 0; q < 14; ++q) m[q] = m[q] + t[q];
         }
-        pl_block_sum<14>(m, red);
+        // the 14 sums and the correspondence hash through one barrier (pl_block_sum's order); the
+        // solve's barrier below separates these reads from the next writes of red / sred
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) hsum += __shfl_xor(hsum, off, 64);
-        if ((tid & 63) == 0) sred[tid >> 6] = (int)hsum;
+        for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+            for (int q = 0; q < 14; ++q) m[q] = m[q] + __shfl_xor(m[q], off, 64);
+            hsum += __shfl_xor(hsum, off, 64);
+        }
+        if ((tid & 63) == 0) {
+#pragma unroll
+            for (int q = 0; q < 14; ++q) red[tid >> 6][q] = m[q];
+            sred[tid >> 6] = (int)hsum;
+        }
         __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 14; ++q) m[q] = (red[0][q] + red[2][q]) + (red[1][q] + red[3][q]);
         const unsigned hash = ((unsigned)sred[0] + (unsigned)sred[1] + (unsigned)sred[2] + (unsigned)sred[3]) & 0x7FFFFFFFu;
-        __syncthreads();
         // the constrained solve once per pair (wave 0), broadcast: on failure x_new keeps what
         // pl_gpc_solve left in it, as in the all-threads version
         if (tid < 64) {
             double xs[3] = {x_new[0], x_new[1], x_new[2]};
             const bool okk = pl_gpc_solve(m, xs);
             if (tid == 0) {
+                s_hash[it] = hash;
                 s_x[0] = xs[0];
                 s_x[1] = xs[1];
                 s_x[2] = xs[2];
@@ -568,8 +581,6 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
         const double co = sdm_cos(x_old[2]), so = sdm_sin(x_old[2]);
         const double ddx = x_new[0] - x_old[0], ddy = x_new[1] - x_old[1];
         const double dl0 = co * ddx + so * ddy, dl1 = -so * ddx + co * ddy, dl2 = pl_angle_diff(x_new[2], x_old[2]);
-        if (tid == 0) s_hash[it] = hash;
-        __syncthreads();
         bool loop = false;
         for (int a = 0; a < it; ++a)
             if (s_hash[a] == hash) loop = true;

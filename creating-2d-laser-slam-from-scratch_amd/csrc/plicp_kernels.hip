@@ -7,10 +7,11 @@
 //                                      reference point inside CSM's polar search interval (reference
 //                                      points resident in LDS), j2 = closer valid neighbour;
 //                     trimming         the two order statistics of the point-to-segment errors by an
-//                                      8-pass radix select on the errors' bit patterns (LDS histograms);
+//                                      radix select on the errors' bit patterns (double-buffered LDS
+//                                      histograms, early settle on a single-key bin);
 //                     doubles          per-reference minimum dist^2 by LDS 64-bit atomicMin on the bits;
 //                     estimate         the 14 point-to-line GPC sums (64-lane xor butterfly, then the
-//                                      4 waves), the constrained 4x4 solve by every thread (bisection on
+//                                      4 waves), the constrained 4x4 solve by wave 0 (bisection on
 //                                      the Lagrange multiplier), oscillation hash, convergence test.
 // The CPU checker oracle/plicp_oracle.c evaluates the same op sequence (-ffp-contract=off here and
 // there), so results agree bit for bit; CSM itself is absent (parity unpinned).
@@ -540,22 +541,12 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
 #pragma unroll
             for (int q = 0; q < 14; ++q) m[q] = m[q] + t[q];
         }
-        // the 14 sums and the correspondence hash through one barrier (pl_block_sum's order); the
-        // solve's barrier below separates these reads from the next writes of red / sred
+        pl_block_sum<14>(m, red);
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-            for (int q = 0; q < 14; ++q) m[q] = m[q] + __shfl_xor(m[q], off, 64);
-            hsum += __shfl_xor(hsum, off, 64);
-        }
-        if ((tid & 63) == 0) {
-#pragma unroll
-            for (int q = 0; q < 14; ++q) red[tid >> 6][q] = m[q];
-            sred[tid >> 6] = (int)hsum;
-        }
+        for (int off = 32; off >= 1; off >>= 1) hsum += __shfl_xor(hsum, off, 64);
+        if ((tid & 63) == 0) sred[tid >> 6] = (int)hsum;
         __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 14; ++q) m[q] = (red[0][q] + red[2][q]) + (red[1][q] + red[3][q]);
+        // the solve's barrier below separates this read from the next write of sred
         const unsigned hash = ((unsigned)sred[0] + (unsigned)sred[1] + (unsigned)sred[2] + (unsigned)sred[3]) & 0x7FFFFFFFu;
         // the constrained solve once per pair (wave 0), broadcast: on failure x_new keeps what
         // pl_gpc_solve left in it, as in the all-threads version

@@ -386,7 +386,11 @@ __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, con
 
 constexpr int MATCH_REG_PTS = 5;  // points per thread kept in registers: scans of up to 1280 points
 
-__global__ void __launch_bounds__(MATCH_THREADS)
+// register budget knob: waves per SIMD the compiler must fit the match kernel into (1 = unconstrained)
+#ifndef S2D_MATCH_WAVES
+#define S2D_MATCH_WAVES 1
+#endif
+__global__ void __launch_bounds__(MATCH_THREADS) __attribute__((amdgpu_waves_per_eu(S2D_MATCH_WAVES)))
 hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__restrict__ state,
                 const float2 *__restrict__ xy, int xy_stride, const int *__restrict__ counts,
                 const float2 *__restrict__ origo, const float *__restrict__ hints, int stream_begin, int mode,

@@ -305,6 +305,7 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
             pl_interval(p, wx, wy, n, min_theta, max_theta, from, to);
             int b1 = -1;
             double best = 0.0;
+            bool searched = false;
             {
                 // Prune the interval to the reference points that can pass the maxd2 test: a point at
                 // polar angle theta_j is at least |w| sin|theta_w - theta_j| from w, so beyond
@@ -323,40 +324,44 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                     const int m = (int)ceil(dth / angle_inc) + 3;
                     from = from > cw - m ? from : cw - m;
                     to = to < cw + m ? to : cw + m;
-                    // Tighter still: the best distance among the 5 cells around the point's own cell
+                    // Tighter still: the best distance among the 9 cells around the point's own cell
                     // bounds the winner, so the same argument with lim = 1.01 sqrt(that) shrinks the
                     // window further (every point left out is > that distance, hence not the minimum).
-                    const int cf = from > cw - 2 ? from : cw - 2, ct = to < cw + 2 ? to : cw + 2;
-                    double bc = maxd2;
-                    bool found = false;
+                    // When the shrunk window lies inside those 9 cells, their first-index argmin is
+                    // already the exhaustive search's answer (all ties sit inside the window).
+                    const int cf = from > cw - 4 ? from : cw - 4, ct = to < cw + 4 ? to : cw + 4;
                     for (int j = cf; j <= ct; ++j) {
                         const double2 q = rpt[j];
                         const double dx = wx - q.x, dy = wy - q.y;
                         const double dist = dx * dx + dy * dy;
-                        if (dist <= bc) {
-                            bc = dist;
-                            found = true;
+                        if (dist > maxd2) continue;
+                        if (b1 == -1 || dist < best) {
+                            b1 = j;
+                            best = dist;
                         }
                     }
-                    if (found) {
-                        const double sn2 = 1.01 * sqrt(bc) / norm;
+                    if (b1 != -1) {
+                        const double sn2 = 1.01 * sqrt(best) / norm;
                         const double dth2 = sdm_atan(sn2 / sqrt(1.0 - sn2 * sn2));
                         const int m2 = (int)ceil(dth2 / angle_inc) + 3;
                         from = from > cw - m2 ? from : cw - m2;
                         to = to < cw + m2 ? to : cw + m2;
+                        if (from >= cf && to <= ct) searched = true;
+                        else b1 = -1;
                     }
                 }
             }
-            for (int j = from; j <= to; ++j) {
-                const double2 q = rpt[j];
-                const double dx = wx - q.x, dy = wy - q.y;
-                const double dist = dx * dx + dy * dy;
-                if (dist > maxd2) continue;
-                if (b1 == -1 || dist < best) {
-                    b1 = j;
-                    best = dist;
+            if (!searched)
+                for (int j = from; j <= to; ++j) {
+                    const double2 q = rpt[j];
+                    const double dx = wx - q.x, dy = wy - q.y;
+                    const double dist = dx * dx + dy * dy;
+                    if (dist > maxd2) continue;
+                    if (b1 == -1 || dist < best) {
+                        b1 = j;
+                        best = dist;
+                    }
                 }
-            }
             if (b1 == -1 || b1 == 0 || b1 == n - 1) continue;   // no match / extrema
             const int up = rup[b1], dn = rdn[b1];
             if (up == -1 && dn == -1) continue;

@@ -343,7 +343,9 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                     if (b1 != -1) {
                         const double sn2 = 1.01 * sqrt(best) / norm;
                         const double dth2 = sdm_atan(sn2 / sqrt(1.0 - sn2 * sn2));
-                        const int m2 = (int)ceil(dth2 / angle_inc) + 3;
+                        // a cell j with |j - cw| > m2 is at least m2 cells of angle away from w (w lies
+                        // inside cell cw), so ceil(dth2 / inc) would do; +1 covers cw's rounding, +1 margin
+                        const int m2 = (int)ceil(dth2 / angle_inc) + 2;
                         from = from > cw - m2 ? from : cw - m2;
                         to = to < cw + m2 ? to : cw + m2;
                         if (from >= cf && to <= ct) searched = true;

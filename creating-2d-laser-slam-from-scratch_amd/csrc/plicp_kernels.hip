@@ -28,6 +28,9 @@ constexpr int PL_THREADS = 256;
 constexpr int PL_RPT_MAX = 8;                   // rays per thread: max_rays <= 2048
 constexpr int PL_MAX_RAYS = PL_THREADS * PL_RPT_MAX;
 constexpr int PL_MAX_IT = 64;
+#ifndef PL_CORE
+#define PL_CORE 4   // half-width of the core search around a point's own cell
+#endif
 
 __device__ __forceinline__ double pl_dist_to_segment(double ax, double ay, double bx, double by, double x, double y)
 {
@@ -329,7 +332,7 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                     // window further (every point left out is > that distance, hence not the minimum).
                     // When the shrunk window lies inside those 9 cells, their first-index argmin is
                     // already the exhaustive search's answer (all ties sit inside the window).
-                    const int cf = from > cw - 4 ? from : cw - 4, ct = to < cw + 4 ? to : cw + 4;
+                    const int cf = from > cw - PL_CORE ? from : cw - PL_CORE, ct = to < cw + PL_CORE ? to : cw + PL_CORE;
                     for (int j = cf; j <= ct; ++j) {
                         const double2 q = rpt[j];
                         const double dx = wx - q.x, dy = wy - q.y;

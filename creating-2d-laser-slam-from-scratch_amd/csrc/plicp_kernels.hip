@@ -318,20 +318,16 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                 const double norm = sqrt(wx * wx + wy * wy);
                 const double lim = 1.01 * p.max_correspondence_dist;
                 if (norm > 2.0 * lim && angle_inc > 0.0) {
-                    const double sn_ = lim / norm;
-                    const double dth = sdm_atan(sn_ / sqrt(1.0 - sn_ * sn_));
                     double th = sdm_atan2(wy, wx);
                     if (th < min_theta) th += 2.0 * SDM_PI;
                     if (th > max_theta) th -= 2.0 * SDM_PI;
                     const int cw = (int)((th - min_theta) / angle_inc);
-                    const int m = (int)ceil(dth / angle_inc) + 3;
-                    from = from > cw - m ? from : cw - m;
-                    to = to < cw + m ? to : cw + m;
                     // Tighter still: the best distance among the 9 cells around the point's own cell
                     // bounds the winner, so the same argument with lim = 1.01 sqrt(that) shrinks the
                     // window further (every point left out is > that distance, hence not the minimum).
                     // When the shrunk window lies inside those 9 cells, their first-index argmin is
-                    // already the exhaustive search's answer (all ties sit inside the window).
+                    // already the exhaustive search's answer (all ties sit inside the window).  Only
+                    // when the core holds no candidate is the maxd window above computed.
                     const int cf = from > cw - PL_CORE ? from : cw - PL_CORE, ct = to < cw + PL_CORE ? to : cw + PL_CORE;
                     for (int j = cf; j <= ct; ++j) {
                         const double2 q = rpt[j];
@@ -353,6 +349,12 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                         to = to < cw + m2 ? to : cw + m2;
                         if (from >= cf && to <= ct) searched = true;
                         else b1 = -1;
+                    } else {
+                        const double sn_ = lim / norm;
+                        const double dth = sdm_atan(sn_ / sqrt(1.0 - sn_ * sn_));
+                        const int m = (int)ceil(dth / angle_inc) + 3;
+                        from = from > cw - m ? from : cw - m;
+                        to = to < cw + m ? to : cw + m;
                     }
                 }
             }

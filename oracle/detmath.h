@@ -140,35 +140,35 @@ static inline double odm_exp(double x)
 /* float-in / float-out wrappers: the single rounding point */
 static inline float odm_sinf(float x) { return (float)odm_sin((double)x); }
 static inline float odm_cosf(float x) { return (float)odm_cos((double)x); }
-/* exp for float arguments in IEEE float: the same op sequence as csrc/detmath.h sdm_expf
- * (Cody-Waite by ln2 with a 16-bit hi part, degree-7 Taylor, exact 2^k scaling; <= 1 ulp). */
-static inline float odm_pow2i(int k) /* 2^k, k in [-126, 127] */
-{
-    union { unsigned int u; float f; } v;
-    v.u = (unsigned int)(k + 127) << 23;
-    return v.f;
-}
+/* exp of a float argument as the reference evaluates it: GridMapLogOdds.h:138 calls `exp` on a float
+ * with only <cmath> in scope, which binds the DOUBLE exp (the built reference harness imports
+ * exp@GLIBC, oracle/_ref/libhector_logodds_ref.so), so the value is (float)exp((double)x).  The
+ * double sequence of odm_exp rounded once to float equals it for every float argument (exhaustive
+ * check against the compiled reference header, tests/test_oracle_cpu.py::test_grid_probability_pinned).
+ * Branch-free: the argument is clamped to [-110, 90], where the float result is already 0 / inf at
+ * the ends, so no special case but NaN remains and the GPU keeps its gathers in flight. */
 static inline float odm_expf(float x)
 {
-    /* branch-free (selects only, so the GPU keeps its gathers in flight); the value equals
-     * x != x ? x : x > 88.72284 ? inf : x < -103.97909 ? 0 : p * 2^k (two-step scaling past 2^-126) */
-    const float xc = (x == x) ? ((x > 88.72284f) ? 88.72284f : ((x < -103.97909f) ? -103.97909f : x)) : 0.0f;
-    const float k = floorf(xc * 1.44269502f + 0.5f);
-    float r = xc - k * 0.693145751953125f;
-    r = r - k * 1.42860677e-06f;
-    float p = 1.98412701e-04f;
-    p = 1.38888892e-03f + r * p;
-    p = 8.33333377e-03f + r * p;
-    p = 4.16666679e-02f + r * p;
-    p = 1.66666672e-01f + r * p;
-    p = 0.5f + r * p;
-    p = 1.0f + r * p;
-    p = 1.0f + r * p;
-    const int ki = (int)k;  /* in [-150, 128] */
-    const int k1 = ki > 127 ? 127 : (ki < -126 ? ki + 64 : ki);
-    const float m2 = ki > 127 ? 2.0f : (ki < -126 ? 5.42101086e-20f /* 2^-64 */ : 1.0f);
-    const float res = (p * odm_pow2i(k1)) * m2;
-    return (x != x) ? x : ((x > 88.72284f) ? HUGE_VALF : ((x < -103.97909f) ? 0.0f : res));
+    const double xd = (x == x) ? (x > 90.0f ? 90.0 : (x < -110.0f ? -110.0 : (double)x)) : 0.0;
+    const double k = floor(xd * ODM_INV_LN2 + 0.5);
+    double r = xd - k * ODM_LN2_HI;
+    r = r - k * ODM_LN2_LO;
+    double q = ODM_F13;
+    q = ODM_F12 + r * q;
+    q = ODM_F11 + r * q;
+    q = ODM_F10 + r * q;
+    q = ODM_F9 + r * q;
+    q = ODM_F8 + r * q;
+    q = ODM_F7 + r * q;
+    q = ODM_F6 + r * q;
+    q = ODM_F5 + r * q;
+    q = ODM_F4 + r * q;
+    q = ODM_F3 + r * q;
+    q = ODM_F2 + r * q;
+    q = 1.0 + r * q;
+    q = 1.0 + r * q;
+    const float res = (float)ldexp(q, (int)k);
+    return (x != x) ? x : res;
 }
 
 

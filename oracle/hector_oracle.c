@@ -674,6 +674,15 @@ int ho_ray_cells(int sx, int sy, int x0, int y0, int x1, int y1, unsigned int *o
 float ho_det_sinf(float x) { return odm_sinf(x); }
 float ho_det_cosf(float x) { return odm_cosf(x); }
 float ho_det_expf(float x) { return odm_expf(x); }
+/* getGridProbability (GridMapLogOdds.h:136-140) as the oracle and the kernels evaluate it; pinned
+ * against the compiled reference header by tests/test_oracle_cpu.py::test_grid_probability_pinned */
+float ho_det_prob(float l)
+{
+    const float odds = odm_expf(l);
+    return odds / (odds + 1.0f);
+}
+/* probToLogOdds (GridMapLogOdds.h:153-157) as the oracle evaluates it */
+float ho_det_prob_to_logodds(float p) { return ho_prob_to_logodds(p); }
 
 /* ---- scan ingest: LaserScan -> DataContainer ------------------------------------------------------
  * HectorMappingRos::scanCallback (lesson4/src/hector_mapping/hector_slam.cc:186-198):

@@ -12,6 +12,12 @@ The reference holds no tests, fixtures or known-answer vectors for this path (SU
   Bresenham restatement (ray_cells) and the libm-vs-detmath tolerance tests.
 * ray_cells.npz -- Bresenham cell lists of updateLineBresenhami (OccGridMapBase.h:220-299)
   computed by the pure-Python restatement in this file (independent of the C oracle).
+* ref_hector_logodds.npz -- outputs of the REFERENCE Hector log-odds cell functions
+  (lesson4/include/lesson4/hector_mapping/map/GridMapLogOdds.h, std-only, compiled unmodified into
+  oracle/_ref/libhector_logodds_ref.so by oracle/Makefile): probToLogOdds factors, cell update
+  sequences (updateSetFree / updateUnsetFree / updateSetOccupied / resetGridCell) and
+  getGridProbability on a strided sample of every float log-odds -- the Hector oracle's A9 rows and
+  its probability evaluation are pinned against these.
 * gmapping_ref.npz -- outputs of the REFERENCE GMapping grid headers (lesson4/include/lesson4/
   gmapping/grid/*.h, compiled unmodified into oracle/_ref/libgmapping_ref.so by oracle/Makefile)
   on synthetic scans: the GMapping oracle and the GPU path are pinned against these.
@@ -142,6 +148,55 @@ def gmapping_fixture(rng):
     return out
 
 
+# ------------------------------------------------------------------ Hector log-odds (reference build)
+def hector_logodds_fixture():
+    import ctypes as C
+    R = C.CDLL(os.path.join(HERE, "_ref", "libhector_logodds_ref.so"))
+    R.hlr_prob_to_logodds.restype = C.c_float
+    R.hlr_prob_to_logodds.argtypes = [C.c_float]
+    R.hlr_factors.argtypes = [C.c_float, C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+    R.hlr_apply_ops.restype = C.c_float
+    R.hlr_apply_ops.argtypes = [C.c_float, C.c_int, C.c_void_p, C.c_int, C.c_float, C.c_float, C.POINTER(C.c_int)]
+    R.hlr_grid_probability_n.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong]
+    rng = np.random.default_rng(4711)
+    probs = np.concatenate([np.asarray([0.4, 0.6, 0.9, 0.5, 0.1, 0.99, 0.01, 0.45, 0.55], np.float32),
+                            rng.uniform(0.001, 0.999, 200).astype(np.float32)])
+    p2l = np.asarray([R.hlr_prob_to_logodds(float(p)) for p in probs], np.float32)
+    pairs = np.asarray([(-1.0, -1.0), (0.4, 0.9), (0.4, 0.6), (0.3, 0.7)], np.float32)
+    facs = []
+    for a, b in pairs:
+        lf, lo = C.c_float(), C.c_float()
+        R.hlr_factors(float(a), float(b), C.byref(lf), C.byref(lo))
+        facs.append((lf.value, lo.value))
+    # update sequences: ops 0 setFree, 1 unsetFree, 2 setOccupied, 3 resetGridCell
+    n_seq, max_len = 400, 64
+    starts = np.concatenate([np.asarray([0.0, 49.9, 50.0, 49.99999, -50.0, 48.5], np.float32),
+                             rng.uniform(-60, 60, n_seq - 6).astype(np.float32)])
+    ops = rng.integers(0, 4, (n_seq, max_len)).astype(np.int32)
+    ops[:6] = 2                      # saturating occupied runs from the clamp neighbourhood
+    lens = rng.integers(1, max_len + 1, n_seq).astype(np.int32)
+    lens[:6] = max_len
+    which = rng.integers(0, len(pairs), n_seq).astype(np.int32)
+    final, upd = np.zeros(n_seq, np.float32), np.zeros(n_seq, np.int32)
+    for i in range(n_seq):
+        u = C.c_int()
+        a, b = pairs[which[i]]
+        final[i] = R.hlr_apply_ops(float(starts[i]), 7, ops[i].ctypes.data, int(lens[i]), float(a), float(b),
+                                   C.byref(u))
+        upd[i] = u.value
+    # getGridProbability on every 16384th float bit pattern (both signs) plus specials
+    pos = np.arange(0, 0x7F800001, 16384, dtype=np.uint64)
+    bits = np.concatenate([pos, pos | 0x80000000, np.asarray([0x7F800000, 0xFF800000, 0x7FC00000, 0x80000000,
+                                                              0x00000001, 0x80000001], np.uint64)])
+    xs = bits.astype(np.uint32).view(np.float32).copy()
+    pr = np.zeros_like(xs)
+    R.hlr_grid_probability_n(xs.ctypes.data, pr.ctypes.data, len(xs))
+    return dict(probs=probs, p2l_bits=p2l.view(np.int32), factor_pairs=pairs,
+                factors_bits=np.asarray(facs, np.float32).view(np.int32), seq_start=starts, seq_ops=ops,
+                seq_len=lens, seq_pair=which, seq_final_bits=final.view(np.int32), seq_upd=upd,
+                prob_x_bits=xs.view(np.int32), prob_bits=pr.view(np.int32))
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
     rng = np.random.default_rng(20250212)
@@ -161,6 +216,10 @@ def main():
         np.savez_compressed(os.path.join(GOLD, "gmapping_ref.npz"), **gmapping_fixture(rng))
     else:
         print("oracle/_ref missing: gmapping_ref.npz not regenerated", file=sys.stderr)
+    if os.path.exists(os.path.join(HERE, "_ref", "libhector_logodds_ref.so")):
+        np.savez_compressed(os.path.join(GOLD, "ref_hector_logodds.npz"), **hector_logodds_fixture())
+    else:
+        print("oracle/_ref missing: ref_hector_logodds.npz not regenerated", file=sys.stderr)
     for f in sorted(os.listdir(GOLD)):
         print(f, os.path.getsize(os.path.join(GOLD, f)))
 

@@ -83,7 +83,7 @@ def hector_lib(variant: str = "") -> C.CDLL:
         L.ho_unit_vectors.argtypes = [_i, _f, _f, _p]
         L.ho_ingest.restype = _i
         L.ho_ingest.argtypes = [_i, _p, _p, C.c_double, _f, _p, _f, _f, C.c_double, _f, _f, _f, _p, _p]
-        for n in ("ho_det_sinf", "ho_det_cosf", "ho_det_expf"):
+        for n in ("ho_det_sinf", "ho_det_cosf", "ho_det_expf", "ho_det_prob", "ho_det_prob_to_logodds"):
             getattr(L, n).restype = _f
             getattr(L, n).argtypes = [_f]
         _HL[variant] = L

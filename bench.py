@@ -188,27 +188,29 @@ def cpu_baseline_all_cores(cfg, procs, seconds=6.0, thresholds=(-1.0, -1.0)):
                       "oracle -O3"}
 
 
-def pose_check(cfg, S, gpu_poses, thresholds=(-1.0, -1.0)):
-    """Pose error of the benchmarked GPU streams (device pose log, every step incl. warmup) vs the
-    CPU oracle in the reference's sequential summation order on the same scans -- the metric's
-    'pose RMSE vs ref' -- plus the absolute error against the synthetic ground truth."""
+def pose_check(cfg, S, gpu_poses, streams, thresholds=(-1.0, -1.0)):
+    """Pose error of the logged GPU streams (device pose log slot i = stream streams[i], every step incl.
+    warmup) vs the CPU oracle in the reference's sequential summation order on the same scans -- the
+    metric's 'pose RMSE vs ref' -- plus the absolute error against the synthetic ground truth."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
 
-    n_streams, n_scans = gpu_poses.shape[1], gpu_poses.shape[0]
+    n_scans = gpu_poses.shape[0]
     e, egt = [], []
-    for s in range(n_streams):
+    for i, s in enumerate(streams):
         r = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0)
         r.set_update_factors(0.4, 0.9)
         r.set_thresholds(*thresholds)
         for k in range(n_scans):
             rp, _, _ = r.process(S.points[s, k, : S.counts[s, k]])
-            e.append(gpu_poses[k, s].astype(np.float64) - rp.astype(np.float64))
-            egt.append(gpu_poses[k, s].astype(np.float64) - S.gt[s, k])
+            e.append(gpu_poses[k, i].astype(np.float64) - rp.astype(np.float64))
+            egt.append(gpu_poses[k, i].astype(np.float64) - S.gt[s, k])
         r.close()
     e, egt = np.asarray(e), np.asarray(egt)
     egt[:, 2] = np.arctan2(np.sin(egt[:, 2]), np.cos(egt[:, 2]))
-    return {"streams": n_streams, "scans_per_stream": n_scans,
+    return {"streams": len(streams), "stream_ids": (f"every 64th of {S.points.shape[0]} and the last"
+                                                    if len(streams) > 2 else list(streams)),
+            "scans_per_stream": n_scans,
             "rmse_xy_m": float(np.sqrt(np.mean(e[:, 0] ** 2 + e[:, 1] ** 2))),
             "rmse_theta_rad": float(np.sqrt(np.mean(e[:, 2] ** 2))),
             "max_abs_xy_m": float(np.abs(e[:, :2]).max()), "max_abs_theta_rad": float(np.abs(e[:, 2]).max()),
@@ -585,6 +587,9 @@ def main():
                          "0.4 m / 0.9 rad (reference semantics, reported separately)")
     ap.add_argument("--cpu-cores", type=int, default=16,
                     help="processes for the all-core CPU baseline (one stream each; the GPU box's CPU share is 16)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="hector ranges input: one hs_step_ranges_batch_device call per step instead of one "
+                         "K-step hs_run_ranges_device call")
     ap.add_argument("--input", choices=["ranges", "points"], default="ranges",
                     help="hector: raw LaserScan ranges through the on-device ingest (scanCallback, default) or "
                          "pre-converted DataContainer points")
@@ -637,9 +642,13 @@ def main():
     thr = (0.4, 0.9) if ref_sem else (-1.0, -1.0)
     fleet.set_thresholds(*thr)           # benchmark mode: update every scan; reference: hector_slam.launch
     hs = torch.cuda.current_stream(dev).cuda_stream
-    n_log = min(2, B)
-    d_plog = torch.zeros((T, n_log, 3), dtype=torch.float32, device=dev)
-    fleet.set_pose_log(d_plog.data_ptr(), n_log, T)
+    # pose log: every 64th stream and the last one (the top of the update lists and of the HBM range)
+    log_streams = sorted(set(range(0, B, 64)) | {B - 1})
+    slot_of = np.full(B, -1, np.int32)
+    slot_of[log_streams] = np.arange(len(log_streams), dtype=np.int32)
+    d_slot = torch.from_numpy(slot_of).to(dev)
+    d_plog = torch.zeros((T, len(log_streams), 3), dtype=torch.float32, device=dev)
+    fleet.set_pose_log_slots(d_plog.data_ptr(), d_slot.data_ptr(), len(log_streams), T)
     if from_ranges:
         # the node's filters with the generator's own beam directions as the unit-vector cache, so the
         # device DataContainers equal synth's points (the pose check below replays those)
@@ -651,6 +660,9 @@ def main():
 
         def step(t):
             fleet.step_ranges_device(d_rng[t].data_ptr(), nb, hip_stream=hs)
+
+        def run(t, k):  # k consecutive steps from step t, pipelined inside the library
+            fleet.run_ranges_device(k, d_rng[t].data_ptr(), nb, B * nb, hip_stream=hs)
     else:
         stride = pts.shape[2]
         step_bytes = pts.shape[1] * pts.shape[2] * 8
@@ -658,8 +670,12 @@ def main():
         def step(t):
             fleet.step_device(d_pts.data_ptr() + t * step_bytes, stride, d_cnt[t].data_ptr(), hip_stream=hs)
 
-    for t in range(W):
-        step(t)
+    pipelined = from_ranges and not args.no_pipeline
+    if pipelined:
+        run(0, W)
+    else:
+        for t in range(W):
+            step(t)
     torch.cuda.synchronize()
     fleet.counters(reset=True)
     fleet.kernel_times(reset=True)
@@ -669,8 +685,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for t in range(W, T):
-        step(t)
+    if pipelined:
+        run(W, K)
+    else:
+        for t in range(W, T):
+            step(t)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -715,7 +734,7 @@ def main():
             cpu = cpu_baseline(cfg, thresholds=thr)
             if args.cpu_cores > 1:
                 cpu["all_cores"] = cpu_baseline_all_cores(cfg, args.cpu_cores, thresholds=thr)
-        pose = pose_check(cfg, S, d_plog.cpu().numpy(), thresholds=thr)
+        pose = pose_check(cfg, S, d_plog.cpu().numpy(), log_streams, thresholds=thr)
         out = {"metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K,
                "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
@@ -727,6 +746,10 @@ def main():
                           "map_size": cfg["map_size"], "levels": cfg["levels"], "beams": 1081,
                           "input": ("LaserScan ranges (on-device ingest in the timed region)" if from_ranges
                                     else "DataContainer points"),
+                          "issue": (("hs_run_ranges_device: K steps in one call"
+                                     + (", two fleet halves pipelined (SLAM2D_PIPELINE=1)"
+                                        if os.environ.get("SLAM2D_PIPELINE", "0") not in ("", "0") else ""))
+                                    if pipelined else "one batch call per step"),
                           "parallelism": f"replicas x{world}",
                           "map_updates_per_scan": round(ctr["updates"] / max(B * K, 1), 4)},
                "roofline": roof, "cpu_baseline": cpu, "pose_vs_ref": pose}

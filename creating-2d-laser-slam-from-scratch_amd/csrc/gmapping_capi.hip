@@ -143,7 +143,7 @@ int gm_create(gm_ctx **out, int num_particles, int max_beams, double xmin, doubl
     g.particle_words = (size_t)g.tiles_x * g.tiles_y * GM_TILE_BLOCK_WORDS;
     g.ntiles = g.tiles_x * g.tiles_y;
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamDefault)) != hipSuccess) {
         delete c;
         return gfail(GM_EHIP, "hipStreamCreate", e);
     }

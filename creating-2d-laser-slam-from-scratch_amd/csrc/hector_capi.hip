@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -30,6 +31,8 @@ int fail(int code, const char *what, hipError_t e = hipSuccess)
     }
     return code;
 }
+
+#define LOCK(c) std::lock_guard<std::recursive_mutex> lock_(c->mu)
 
 #define HCHK(expr)                                          \
     do {                                                    \
@@ -61,7 +64,7 @@ struct hs_ctx {
     float *d_out_pose = nullptr;
     float *d_out_cov = nullptr;
     int8_t *d_occ = nullptr;
-    PoseLog plog{nullptr, 0, 0};
+    PoseLog plog{nullptr, 0, 0, nullptr};
     hipStream_t stream = nullptr;
     // timing
     bool timing = false;
@@ -82,10 +85,24 @@ struct hs_ctx {
     int update_single = 1;  // hs_update_kernel (per stream-level, default) or bin + tile kernels
     int ncu = 256;
     bool upd_parts_fixed = false;  // SLAM2D_UPD_PARTS given: no batch-size adaptive split
-    UpdList *wl[2] = {nullptr, nullptr};  // lists of updating streams (hector_internal.h)
-    int wl_parity = 0;
+    // per part (a batch split over part streams): two alternating lists of updating streams
+    // (hector_internal.h UpdList): the match kernel appends to one, the update kernel reads it and
+    // clears the other for the next step
+    UpdList *wl[MAX_PARTS][2] = {};
+    int wl_parity[MAX_PARTS] = {};
     hipStream_t pstream[MAX_PARTS] = {};
     hipEvent_t ev_start = nullptr, ev_done[MAX_PARTS] = {};
+    // hs_run_ranges_device pipeline (SLAM2D_PIPELINE=1): update of one half of the fleet beside the other
+    // half's match.  Measured slower at the north-star size (0.97 M vs 1.04 M scans/s: the update
+    // kernel already fills the CUs, and a concurrent match slows it more than it hides), so off by default.
+    bool pipeline = false;
+    hipEvent_t ev_upd[MAX_PARTS] = {};
+    // the last device work of the context (every *_device call waits for it on its own stream, so the
+    // per-context scratch -- update lists, ingest buffers, queues -- is never used by two streams at once)
+    hipEvent_t ev_last = nullptr;
+    // serialises host calls on one context (e.g. a publish thread's hs_get_map against the spin
+    // thread's hs_update, hector_slam.cc:277 vs :201)
+    std::recursive_mutex mu;
     // scan ingest (hs_set_laser): unit vectors, geometry, the batch's DataContainers
     bool has_laser = false;
     IngestGeom ingest{};
@@ -166,8 +183,10 @@ int reset_all(hs_ctx *c)
     HCHK(hipGetLastError());
     std::vector<StreamState> h(c->B, initial_state());
     HCHK(hipMemcpyAsync(c->d_state, h.data(), sizeof(StreamState) * c->B, hipMemcpyHostToDevice, c->stream));
-    for (int i = 0; i < 2; ++i)
-        if (c->wl[i]) HCHK(hipMemsetAsync(c->wl[i], 0, sizeof(int) * 4, c->stream));
+    for (int p = 0; p < MAX_PARTS; ++p)
+        for (int i = 0; i < 2; ++i)
+            if (c->wl[p][i]) HCHK(hipMemsetAsync(c->wl[p][i], 0, sizeof(int) * 4, c->stream));
+    for (int p = 0; p < MAX_PARTS; ++p) c->wl_parity[p] = 0;
     HCHK(hipStreamSynchronize(c->stream));
     return HS_OK;
 }
@@ -195,7 +214,8 @@ void end_timed(hs_ctx *c, hipStream_t s)
 }
 
 int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int xy_stride, const int *n,
-                const float2 *origo, const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s)
+                const float2 *origo, const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s,
+                hipEvent_t wait_before_update = nullptr)
 {
     WorkQueue *wq = c->d_wq + part;
     uint4 *segs = c->d_segs + (size_t)part * c->seg_cap;
@@ -203,16 +223,17 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     WorkItem *wholes = c->d_wholes + (size_t)part * c->B * c->levels;
     // the single-kernel update consumes the match kernel's list of updating streams (one part only)
     const size_t upd_shmem = sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + (size_t)((c->max_points + 3) & ~3) +
-                                                 4 * (size_t)fan_groups(c->max_points));
+                                                 UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));
     const bool single = c->update_single && upd_shmem <= 65536;
-    const bool use_list = single && c->nparts == 1 && !c->upd_parts_fixed && mode != MODE_MATCH_ONLY;
-    UpdList *wl_cur = use_list ? c->wl[c->wl_parity] : nullptr;
+    const bool use_list = single && !c->upd_parts_fixed && mode != MODE_MATCH_ONLY;
+    UpdList *wl_cur = use_list ? c->wl[part][c->wl_parity[part]] : nullptr;
     begin_timed(c, 0, s);
     hipLaunchKernelGGL(hs_match_kernel, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state, xy,
                        xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur);
     end_timed(c, s);
     HCHK(hipGetLastError());
     if (mode == MODE_MATCH_ONLY) return HS_OK;
+    if (wait_before_update) HCHK(hipStreamWaitEvent(s, wait_before_update, 0));
     // hs_update_kernel keeps the scan's rays in LDS: beyond 64 KB of dynamic LDS (max_points > ~13k)
     // the binned kernels, whose LDS use is independent of the scan size, take over
     if (single && use_list) {
@@ -224,8 +245,8 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
             for (int l = 0; l < c->levels; ++l) b += pl[l] * U;
             blocks = b > blocks ? b : blocks;
         }
-        UpdList *wl_next = c->wl[c->wl_parity ^ 1];
-        c->wl_parity ^= 1;
+        UpdList *wl_next = c->wl[part][c->wl_parity[part] ^ 1];
+        c->wl_parity[part] ^= 1;
         begin_timed(c, 2, s);
         hipLaunchKernelGGL(hs_update_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
                            c->d_state, xy, xy_stride, begin, count, c->max_points, wl_cur, wl_next, c->ncu);
@@ -296,7 +317,37 @@ int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride
     return HS_OK;
 }
 
+// The pipelined run (hs_run_ranges_device) needs the list-driven single update kernel on every part.
+bool pipeline_ok(const hs_ctx *c)
+{
+    const size_t upd_shmem = sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + (size_t)((c->max_points + 3) & ~3) +
+                                                 UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));
+    return c->pipeline && c->update_single && upd_shmem <= 65536 && !c->upd_parts_fixed && c->B >= 2;
+}
+
 int check_stream(hs_ctx *c, int stream) { return (c && stream >= 0 && stream < c->B) ? HS_OK : HS_EINVAL; }
+
+// *_device calls may name any HIP stream: order each call after the context's previous device work
+// (enter) and publish its own (leave), so two calls never share the context's scratch concurrently
+int dev_enter(hs_ctx *c, hipStream_t s)
+{
+    HCHK(hipStreamWaitEvent(s, c->ev_last, 0));
+    return HS_OK;
+}
+int dev_leave(hs_ctx *c, hipStream_t s)
+{
+    HCHK(hipEventRecord(c->ev_last, s));
+    return HS_OK;
+}
+
+int launch_ingest(hs_ctx *c, int count, const float *d_ranges, int range_stride, float2 *d_xy, int xy_stride, int *d_n,
+                  float2 *d_origo, hipStream_t s)
+{
+    hipLaunchKernelGGL(hs_ingest_kernel, dim3(count), dim3(256), 0, s, c->ingest, c->d_cs, d_ranges, range_stride, d_xy,
+                       xy_stride, d_n, d_origo);
+    HCHK(hipGetLastError());
+    return HS_OK;
+}
 
 // Stage one host scan into the single-stream buffers.
 int stage_scan(hs_ctx *c, const float *xy, int n, float ox, float oy, const float *hint)
@@ -345,7 +396,9 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
     c->geom.min_ang = 0.13f * 1.0f;
     c->cells_bytes = sizeof(float) * c->geom.stream_words * (size_t)num_streams;
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+    // blocking streams (not hipStreamNonBlocking): work a caller queued on the legacy default stream
+    // (e.g. torch's default stream zeroing an output) is ordered before the context's own kernels
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamDefault)) != hipSuccess) {
         delete c;
         return fail(HS_EHIP, "hipStreamCreate", e);
     }
@@ -379,6 +432,8 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
             per_cu = 4;
         const char *tg = getenv("SLAM2D_TILE_WG_PER_CU");
         c->tile_grid = ncu * (tg ? atoi(tg) : per_cu);
+        const char *pp = getenv("SLAM2D_PIPELINE");
+        c->pipeline = pp && atoi(pp) != 0;
         const char *np = getenv("SLAM2D_PARTS");
         c->nparts = np ? atoi(np) : 1;
         const char *um = getenv("SLAM2D_UPDATE");
@@ -405,14 +460,16 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         else c->seg_cap = (unsigned)((size_t)c->seg_cap / c->nparts + (1u << 16));
         if (const char *e2 = getenv("SLAM2D_ITEM_CAP")) c->item_cap = (unsigned)atoll(e2);
         else c->item_cap = (unsigned)((size_t)c->item_cap / c->nparts + (1u << 10));
-        for (int p = 0; p < c->nparts; ++p) {
-            if ((e = hipStreamCreateWithFlags(&c->pstream[p], hipStreamNonBlocking)) != hipSuccess ||
-                (e = hipEventCreateWithFlags(&c->ev_done[p], hipEventDisableTiming)) != hipSuccess) {
+        for (int p = 0; p < MAX_PARTS; ++p) {
+            if ((e = hipStreamCreateWithFlags(&c->pstream[p], hipStreamDefault)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&c->ev_done[p], hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&c->ev_upd[p], hipEventDisableTiming)) != hipSuccess) {
                 hs_destroy(c);
                 return fail(HS_EHIP, "hipStreamCreate(part)", e);
             }
         }
-        if ((e = hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming)) != hipSuccess) {
+        if ((e = hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming)) != hipSuccess) {
             hs_destroy(c);
             return fail(HS_EHIP, "hipEventCreate", e);
         }
@@ -421,12 +478,16 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         (e = hipMalloc(&c->d_segs, sizeof(uint4) * (size_t)c->seg_cap * c->nparts)) != hipSuccess ||
         (e = hipMalloc(&c->d_items, sizeof(WorkItem) * (size_t)c->item_cap * c->nparts)) != hipSuccess ||
         (e = hipMalloc(&c->d_wholes, sizeof(WorkItem) * (size_t)num_streams * levels * c->nparts)) != hipSuccess ||
-        (e = hipMalloc(&c->d_wq, sizeof(WorkQueue) * c->nparts)) != hipSuccess ||
-        (e = hipMalloc(&c->wl[0], sizeof(int) * (4 + (size_t)num_streams))) != hipSuccess ||
-        (e = hipMalloc(&c->wl[1], sizeof(int) * (4 + (size_t)num_streams))) != hipSuccess) {
+        (e = hipMalloc(&c->d_wq, sizeof(WorkQueue) * c->nparts)) != hipSuccess) {
         hs_destroy(c);
         return fail(HS_ENOMEM, "hipMalloc", e);
     }
+    for (int p = 0; p < MAX_PARTS; ++p)
+        for (int i = 0; i < 2; ++i)
+            if ((e = hipMalloc(&c->wl[p][i], sizeof(int) * (4 + (size_t)num_streams))) != hipSuccess) {
+                hs_destroy(c);
+                return fail(HS_ENOMEM, "hipMalloc(update list)", e);
+            }
     {
         WorkQueue q;
         memset(&q, 0, sizeof(q));
@@ -451,7 +512,7 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
 int hs_destroy(hs_ctx *c)
 {
     if (!c) return HS_OK;
-    if (c->stream) hipStreamSynchronize(c->stream);
+    hipDeviceSynchronize();  // device work of the context may be on any stream (*_device calls)
     hipFree(c->d_cells);
     hipFree(c->d_state);
     hipFree(c->d_pts1);
@@ -466,8 +527,8 @@ int hs_destroy(hs_ctx *c)
     hipFree(c->d_items);
     hipFree(c->d_wholes);
     hipFree(c->d_wq);
-    hipFree(c->wl[0]);
-    hipFree(c->wl[1]);
+    for (int p = 0; p < MAX_PARTS; ++p)
+        for (int i = 0; i < 2; ++i) hipFree(c->wl[p][i]);
     hipFree(c->d_cs);
     hipFree(c->d_ixy);
     hipFree(c->d_in);
@@ -484,8 +545,10 @@ int hs_destroy(hs_ctx *c)
     for (int p = 0; p < MAX_PARTS; ++p) {
         if (c->pstream[p]) hipStreamDestroy(c->pstream[p]);
         if (c->ev_done[p]) hipEventDestroy(c->ev_done[p]);
+        if (c->ev_upd[p]) hipEventDestroy(c->ev_upd[p]);
     }
     if (c->ev_start) hipEventDestroy(c->ev_start);
+    if (c->ev_last) hipEventDestroy(c->ev_last);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return HS_OK;
@@ -494,12 +557,15 @@ int hs_destroy(hs_ctx *c)
 int hs_reset(hs_ctx *c)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    LOCK(c);
+    HCHK(hipDeviceSynchronize());
     return reset_all(c);
 }
 
 int hs_set_update_factors(hs_ctx *c, float free_factor, float occupied_factor)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    LOCK(c);
     c->geom.lf = prob_to_logodds(free_factor);
     c->geom.lo = prob_to_logodds(occupied_factor);
     return HS_OK;
@@ -508,6 +574,7 @@ int hs_set_update_factors(hs_ctx *c, float free_factor, float occupied_factor)
 int hs_set_map_update_thresholds(hs_ctx *c, float min_dist, float min_angle)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    LOCK(c);
     c->geom.min_dist = min_dist;
     c->geom.min_ang = min_angle;
     return HS_OK;
@@ -546,10 +613,13 @@ int hs_update(hs_ctx *c, int stream, const float *xy, int n, float ox, float oy,
               int map_without_matching, float pose_out[3], float cov_out[9], int *did_update_out)
 {
     if (check_stream(c, stream) != HS_OK) return fail(HS_EINVAL, "bad ctx/stream");
-    int rc = stage_scan(c, xy, n, ox, oy, hint);
+    LOCK(c);
+    int rc = dev_enter(c, c->stream);
+    if (rc == HS_OK) rc = stage_scan(c, xy, n, ox, oy, hint);
     if (rc != HS_OK) return rc;
     rc = launch_step(c, stream, 1, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, hint ? c->d_hint1 : nullptr,
                      map_without_matching ? MODE_NO_MATCH_FORCE : MODE_PROCESS, c->d_out_pose, c->d_out_cov, c->stream);
+    if (rc == HS_OK) rc = dev_leave(c, c->stream);
     if (rc != HS_OK) return rc;
     StreamState st;
     HCHK(hipMemcpyAsync(&st, c->d_state + stream, sizeof(st), hipMemcpyDeviceToHost, c->stream));
@@ -564,10 +634,13 @@ int hs_match(hs_ctx *c, int stream, const float *xy, int n, float ox, float oy, 
              float cov_out[9])
 {
     if (check_stream(c, stream) != HS_OK || !hint) return fail(HS_EINVAL, "bad ctx/stream/hint");
-    int rc = stage_scan(c, xy, n, ox, oy, hint);
+    LOCK(c);
+    int rc = dev_enter(c, c->stream);
+    if (rc == HS_OK) rc = stage_scan(c, xy, n, ox, oy, hint);
     if (rc != HS_OK) return rc;
     rc = launch_step(c, stream, 1, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, c->d_hint1, MODE_MATCH_ONLY,
                      c->d_out_pose, c->d_out_cov, c->stream);
+    if (rc == HS_OK) rc = dev_leave(c, c->stream);
     if (rc != HS_OK) return rc;
     float p[3], cv[9];
     HCHK(hipMemcpyAsync(p, c->d_out_pose, sizeof(p), hipMemcpyDeviceToHost, c->stream));
@@ -581,10 +654,13 @@ int hs_match(hs_ctx *c, int stream, const float *xy, int n, float ox, float oy, 
 int hs_update_by_scan(hs_ctx *c, int stream, const float *xy, int n, float ox, float oy, const float pose[3])
 {
     if (check_stream(c, stream) != HS_OK || !pose) return fail(HS_EINVAL, "bad ctx/stream/pose");
-    int rc = stage_scan(c, xy, n, ox, oy, pose);
+    LOCK(c);
+    int rc = dev_enter(c, c->stream);
+    if (rc == HS_OK) rc = stage_scan(c, xy, n, ox, oy, pose);
     if (rc != HS_OK) return rc;
     rc = launch_step(c, stream, 1, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, c->d_hint1, MODE_UPDATE_ONLY,
                      nullptr, nullptr, c->stream);
+    if (rc == HS_OK) rc = dev_leave(c, c->stream);
     if (rc != HS_OK) return rc;
     HCHK(hipStreamSynchronize(c->stream));
     return HS_OK;
@@ -593,6 +669,8 @@ int hs_update_by_scan(hs_ctx *c, int stream, const float *xy, int n, float ox, f
 int hs_get_last_pose(hs_ctx *c, int stream, float pose_out[3], float cov_out[9])
 {
     if (check_stream(c, stream) != HS_OK) return fail(HS_EINVAL, "bad ctx/stream");
+    LOCK(c);
+    if (dev_enter(c, c->stream) != HS_OK) return HS_EHIP;
     StreamState st;
     HCHK(hipMemcpyAsync(&st, c->d_state + stream, sizeof(st), hipMemcpyDeviceToHost, c->stream));
     HCHK(hipStreamSynchronize(c->stream));
@@ -605,6 +683,8 @@ int hs_get_map(hs_ctx *c, int stream, int level, int8_t *occ_out, float *logodds
                int *update_index_out)
 {
     if (check_stream(c, stream) != HS_OK || level < 0 || level >= c->levels) return fail(HS_EINVAL, "bad stream/level");
+    LOCK(c);
+    if (dev_enter(c, c->stream) != HS_OK) return HS_EHIP;
     const LevelGeom &L = c->geom.lv[level];
     const size_t ncell = (size_t)L.sx * L.sy;
     const size_t nwords = (size_t)L.tiles_x * L.tiles_y * TILE_BLOCK_WORDS;
@@ -638,6 +718,8 @@ int hs_set_map(hs_ctx *c, int stream, int level, const float *logodds, const int
 {
     if (check_stream(c, stream) != HS_OK || level < 0 || level >= c->levels || !logodds || !upd)
         return fail(HS_EINVAL, "bad arguments");
+    LOCK(c);
+    if (dev_enter(c, c->stream) != HS_OK) return HS_EHIP;
     const LevelGeom &L = c->geom.lv[level];
     const size_t nwords = (size_t)L.tiles_x * L.tiles_y * TILE_BLOCK_WORDS;
     float *base = c->d_cells + (size_t)stream * c->geom.stream_words + L.word_offset;
@@ -661,9 +743,64 @@ int hs_step_batch_device(hs_ctx *c, int stream_begin, int count, const float *d_
     if (!c || stream_begin < 0 || count < 0 || stream_begin + count > c->B || !d_xy || !d_n ||
         xy_stride < c->max_points)
         return fail(HS_EINVAL, "bad batch arguments (xy_stride must be >= max_points)");
+    LOCK(c);
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-    return launch_step(c, stream_begin, count, (const float2 *)d_xy, xy_stride, d_n, (const float2 *)d_origo, d_hints,
-                       MODE_PROCESS, nullptr, nullptr, s);
+    int rc = dev_enter(c, s);
+    if (rc == HS_OK)
+        rc = launch_step(c, stream_begin, count, (const float2 *)d_xy, xy_stride, d_n, (const float2 *)d_origo, d_hints,
+                         MODE_PROCESS, nullptr, nullptr, s);
+    return rc == HS_OK ? dev_leave(c, s) : rc;
+}
+
+int hs_run_ranges_device(hs_ctx *c, int steps, const float *d_ranges, int range_stride, size_t step_stride,
+                         void *hip_stream)
+{
+    if (!c || steps < 0 || (steps > 0 && !d_ranges)) return fail(HS_EINVAL, "bad run arguments");
+    LOCK(c);
+    if (!c->has_laser) return fail(HS_EINVAL, "hs_set_laser not called");
+    if (range_stride < c->ingest.n || step_stride < (size_t)range_stride * c->B)
+        return fail(HS_EINVAL, "range_stride < n_beams or step_stride < num_streams * range_stride");
+    if (steps == 0) return HS_OK;
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    int rc = dev_enter(c, s);
+    if (rc != HS_OK) return rc;
+    if (!pipeline_ok(c)) {  // default: the steps in order on s
+        for (int k = 0; k < steps && rc == HS_OK; ++k) {
+            rc = launch_ingest(c, c->B, d_ranges + (size_t)k * step_stride, range_stride, c->d_ixy, c->max_points, c->d_in,
+                               c->d_iorigo, s);
+            if (rc == HS_OK)
+                rc = launch_step(c, 0, c->B, c->d_ixy, c->max_points, c->d_in, c->d_iorigo, nullptr, MODE_PROCESS, nullptr,
+                                 nullptr, s);
+        }
+        return rc == HS_OK ? dev_leave(c, s) : rc;
+    }
+    // Two halves of the fleet on part streams 0 / 1.  Per step and half: ingest, match, then the grid
+    // update once the OTHER half's previous update has finished, so that the updates alternate and each
+    // one runs beside the other half's match:  U_A(k) || M_B(k),  U_B(k) || M_A(k+1).  Streams are
+    // independent, so the results equal the in-order steps bit for bit.
+    const int h0 = (c->B + 1) / 2;
+    const int beg[2] = {0, h0}, cnt[2] = {h0, c->B - h0};
+    HCHK(hipEventRecord(c->ev_start, s));
+    for (int h = 0; h < 2; ++h) HCHK(hipStreamWaitEvent(c->pstream[h], c->ev_start, 0));
+    for (int k = 0; k < steps && rc == HS_OK; ++k) {
+        const float *rk = d_ranges + (size_t)k * step_stride;
+        for (int h = 0; h < 2 && rc == HS_OK; ++h) {
+            hipStream_t ps = c->pstream[h];
+            float2 *xy = c->d_ixy + (size_t)beg[h] * c->max_points;
+            rc = launch_ingest(c, cnt[h], rk + (size_t)beg[h] * range_stride, range_stride, xy, c->max_points,
+                               c->d_in + beg[h], c->d_iorigo + beg[h], ps);
+            if (rc != HS_OK) break;
+            hipEvent_t wait = (h == 1 || k > 0) ? c->ev_upd[h ^ 1] : nullptr;
+            rc = launch_part(c, h, beg[h], cnt[h], xy, c->max_points, c->d_in + beg[h], c->d_iorigo + beg[h], nullptr,
+                             MODE_PROCESS, nullptr, nullptr, ps, wait);
+            if (rc == HS_OK && hipEventRecord(c->ev_upd[h], ps) != hipSuccess) rc = fail(HS_EHIP, "hipEventRecord");
+        }
+    }
+    for (int h = 0; h < 2; ++h) {
+        HCHK(hipEventRecord(c->ev_done[h], c->pstream[h]));
+        HCHK(hipStreamWaitEvent(s, c->ev_done[h], 0));
+    }
+    return rc == HS_OK ? dev_leave(c, s) : rc;
 }
 
 void hs_default_laser(hs_laser *L, int n_beams, float angle_min, float angle_increment)
@@ -686,6 +823,7 @@ void hs_default_laser(hs_laser *L, int n_beams, float angle_min, float angle_inc
 int hs_set_laser(hs_ctx *c, const hs_laser *L, const double *unit_vectors)
 {
     if (!c || !L) return fail(HS_EINVAL, "NULL argument");
+    LOCK(c);
     if (L->n_beams < 0 || L->n_beams > c->max_points) return fail(HS_EINVAL, "n_beams must be in [0, max_points]");
     IngestGeom &g = c->ingest;
     g.n = L->n_beams;
@@ -720,6 +858,7 @@ int hs_set_laser(hs_ctx *c, const hs_laser *L, const double *unit_vectors)
             (e = hipMalloc(&c->d_ranges1, sizeof(float) * (size_t)c->max_points)) != hipSuccess)
             return fail(HS_ENOMEM, "hipMalloc(ingest)", e);
     }
+    if (dev_enter(c, c->stream) != HS_OK) return HS_EHIP;
     if (L->n_beams > 0)
         HCHK(hipMemcpyAsync(c->d_cs, cs.data(), sizeof(double2) * L->n_beams, hipMemcpyHostToDevice, c->stream));
     HCHK(hipStreamSynchronize(c->stream));
@@ -731,41 +870,49 @@ int hs_ingest_batch_device(hs_ctx *c, int count, const float *d_ranges, int rang
                            int *d_n, float *d_origo, void *hip_stream)
 {
     if (!c || count < 0 || (count > 0 && (!d_ranges || !d_xy || !d_n))) return fail(HS_EINVAL, "bad ingest arguments");
+    LOCK(c);
     if (!c->has_laser) return fail(HS_EINVAL, "hs_set_laser not called");
     if (range_stride < c->ingest.n || xy_stride < c->ingest.n) return fail(HS_EINVAL, "stride < n_beams");
     if (count == 0) return HS_OK;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-    hipLaunchKernelGGL(hs_ingest_kernel, dim3(count), dim3(256), 0, s, c->ingest, c->d_cs, d_ranges, range_stride,
-                       (float2 *)d_xy, xy_stride, d_n, (float2 *)d_origo);
-    HCHK(hipGetLastError());
-    return HS_OK;
+    int rc = dev_enter(c, s);
+    if (rc == HS_OK) rc = launch_ingest(c, count, d_ranges, range_stride, (float2 *)d_xy, xy_stride, d_n, (float2 *)d_origo, s);
+    return rc == HS_OK ? dev_leave(c, s) : rc;
 }
 
 int hs_step_ranges_batch_device(hs_ctx *c, int stream_begin, int count, const float *d_ranges, int range_stride,
                                 const float *d_hints, void *hip_stream)
 {
     if (!c || stream_begin < 0 || count < 0 || stream_begin + count > c->B) return fail(HS_EINVAL, "bad batch arguments");
+    LOCK(c);
+    if (!c->has_laser) return fail(HS_EINVAL, "hs_set_laser not called");
+    if (count > 0 && !d_ranges) return fail(HS_EINVAL, "d_ranges is NULL");
+    if (range_stride < c->ingest.n) return fail(HS_EINVAL, "range_stride < n_beams");
+    if (count == 0) return HS_OK;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-    int rc = hs_ingest_batch_device(c, count, d_ranges, range_stride, (float *)c->d_ixy, c->max_points, c->d_in,
-                                    (float *)c->d_iorigo, s);
-    if (rc != HS_OK || count == 0) return rc;
-    return launch_step(c, stream_begin, count, c->d_ixy, c->max_points, c->d_in, c->d_iorigo, d_hints, MODE_PROCESS,
-                       nullptr, nullptr, s);
+    int rc = dev_enter(c, s);
+    if (rc == HS_OK) rc = launch_ingest(c, count, d_ranges, range_stride, c->d_ixy, c->max_points, c->d_in, c->d_iorigo, s);
+    if (rc == HS_OK)
+        rc = launch_step(c, stream_begin, count, c->d_ixy, c->max_points, c->d_in, c->d_iorigo, d_hints, MODE_PROCESS,
+                         nullptr, nullptr, s);
+    return rc == HS_OK ? dev_leave(c, s) : rc;
 }
 
 int hs_update_ranges(hs_ctx *c, int stream, const float *ranges, float pose_out[3], float cov_out[9], int *did_update_out)
 {
     if (check_stream(c, stream) != HS_OK) return fail(HS_EINVAL, "bad ctx/stream");
+    LOCK(c);
     if (!c->has_laser) return fail(HS_EINVAL, "hs_set_laser not called");
     if (c->ingest.n > 0 && !ranges) return fail(HS_EINVAL, "ranges is NULL");
+    if (dev_enter(c, c->stream) != HS_OK) return HS_EHIP;
     if (c->ingest.n > 0)
         HCHK(hipMemcpyAsync(c->d_ranges1, ranges, sizeof(float) * c->ingest.n, hipMemcpyHostToDevice, c->stream));
-    int rc = hs_ingest_batch_device(c, 1, c->d_ranges1, c->max_points, (float *)c->d_pts1, c->max_points, c->d_n1,
-                                    (float *)c->d_origo1, c->stream);
+    int rc = launch_ingest(c, 1, c->d_ranges1, c->max_points, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, c->stream);
     if (rc != HS_OK) return rc;
     // scanCallback: startEstimate = getLastScanMatchPose() (hector_slam.cc:201), i.e. no explicit hint
     rc = launch_step(c, stream, 1, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, nullptr, MODE_PROCESS, c->d_out_pose,
                      c->d_out_cov, c->stream);
+    if (rc == HS_OK) rc = dev_leave(c, c->stream);
     if (rc != HS_OK) return rc;
     StreamState st;
     HCHK(hipMemcpyAsync(&st, c->d_state + stream, sizeof(st), hipMemcpyDeviceToHost, c->stream));
@@ -779,6 +926,7 @@ int hs_update_ranges(hs_ctx *c, int stream, const float *ranges, float pose_out[
 int hs_get_poses(hs_ctx *c, float *poses_out, float *covs_out, int *did_update_out, int64_t *cells_out)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    LOCK(c);
     std::vector<StreamState> h(c->B);
     HCHK(hipDeviceSynchronize());
     HCHK(hipMemcpy(h.data(), c->d_state, sizeof(StreamState) * c->B, hipMemcpyDeviceToHost));
@@ -794,6 +942,7 @@ int hs_get_poses(hs_ctx *c, float *poses_out, float *covs_out, int *did_update_o
 int hs_get_counters(hs_ctx *c, int64_t out[6], int reset)
 {
     if (!c || !out) return fail(HS_EINVAL, "NULL argument");
+    LOCK(c);
     std::vector<StreamState> h(c->B);
     HCHK(hipStreamSynchronize(c->stream));
     HCHK(hipDeviceSynchronize());
@@ -818,6 +967,7 @@ int hs_get_counters(hs_ctx *c, int64_t out[6], int reset)
 int hs_get_queue_stats(hs_ctx *c, int64_t out[8], int reset_stamps)
 {
     if (!c || !out) return fail(HS_EINVAL, "NULL argument");
+    LOCK(c);
     WorkQueue q[MAX_PARTS];
     unsigned long long st[8];
     HCHK(hipDeviceSynchronize());
@@ -831,9 +981,6 @@ int hs_get_queue_stats(hs_ctx *c, int64_t out[8], int reset_stamps)
         out[3] += q[p].overflow;
     }
     for (int k = 0; k < 4; ++k) out[4 + k] = (int64_t)st[k];
-#ifdef S2D_VISITS
-    for (int k = 0; k < 4; ++k) out[k] = (int64_t)st[4 + k];  // diagnostic build: raster visit counters
-#endif
     if (reset_stamps) {
         memset(st, 0, sizeof(st));
         HCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), st, sizeof(st)));
@@ -853,9 +1000,22 @@ int hs_get_device_buffers(hs_ctx *c, void **cells, size_t *cells_bytes, size_t *
 int hs_set_pose_log(hs_ctx *c, float *d_buf, int streams, int capacity)
 {
     if (!c || streams < 0 || capacity < 0 || (d_buf && streams > c->B)) return fail(HS_EINVAL, "bad pose log");
+    LOCK(c);
     c->plog.buf = d_buf;
     c->plog.streams = d_buf ? streams : 0;
     c->plog.capacity = d_buf ? capacity : 0;
+    c->plog.slot_of = nullptr;
+    return HS_OK;
+}
+
+int hs_set_pose_log_slots(hs_ctx *c, float *d_buf, const int *d_slot_of_stream, int slots, int capacity)
+{
+    if (!c || slots < 0 || capacity < 0 || (d_buf && !d_slot_of_stream)) return fail(HS_EINVAL, "bad pose log");
+    LOCK(c);
+    c->plog.buf = d_buf;
+    c->plog.streams = d_buf ? slots : 0;
+    c->plog.capacity = d_buf ? capacity : 0;
+    c->plog.slot_of = d_buf ? d_slot_of_stream : nullptr;
     return HS_OK;
 }
 
@@ -864,6 +1024,7 @@ void *hs_get_stream(hs_ctx *c) { return c ? (void *)c->stream : nullptr; }
 int hs_set_timing(hs_ctx *c, int enable)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    LOCK(c);
     c->timing = enable != 0;
     return HS_OK;
 }
@@ -871,6 +1032,7 @@ int hs_set_timing(hs_ctx *c, int enable)
 int hs_get_kernel_times(hs_ctx *c, double ms_out[3], int64_t launches_out[3], int reset)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    LOCK(c);
     for (auto &p : c->ev_used) {
         HCHK(hipEventSynchronize(p.b));
         float ms = 0.0f;

@@ -128,9 +128,10 @@ inline __host__ __device__ void upd_split(int U, int ncu, int levels, int *parts
 
 // Optional device pose log: the match kernel appends every step's pose of streams [0, streams).
 struct PoseLog {
-    float *buf;    // [capacity][streams][3]
-    int streams;
+    float *buf;          // [capacity][streams][3]
+    int streams;         // slots per row
     int capacity;
+    const int *slot_of;  // device [B]: slot of stream s (< 0: not logged); NULL: stream s -> slot s
 };
 
 }  // namespace s2d

@@ -12,21 +12,21 @@
 // One step = one HectorSlamProcessor::update per stream (H/slam_main/HectorSlamProcessor.h:81-108):
 //   k1 hs_match_kernel      one 256-thread workgroup per stream: all levels coarse->fine, all
 //                           Gauss-Newton iterations, block reduction of H/b, 3x3 solve, gating.
-//   k2 hs_update_kernel     one 256-thread workgroup per (stream, level): the scan's bounding box is
-//                           walked in 64x64-cell tiles; each ray's cells inside a tile come from the
-//                           closed-form Bresenham step range, the once-per-scan semantics of
-//                           bresenhamCellFree/Occ (H/map/OccGridMapBase.h:302-330) are resolved in
-//                           LDS, then touched cells get ONE coalesced 8-byte read-modify-write.
-//                           No global atomics; see DESIGN.md "once-per-scan semantics".
+//   k2 hs_update_kernel     256-thread workgroups per (stream, level, part): the tiles of the scan's
+//                           bounding box (64 x 32 cells, the storage tile) are dealt round-robin to
+//                           the level's parts (split by the number of updating streams, upd_split);
+//                           each ray's cells inside a tile come from the closed-form Bresenham step
+//                           range, the once-per-scan semantics of bresenhamCellFree/Occ
+//                           (H/map/OccGridMapBase.h:302-330) are resolved in LDS event words, then
+//                           every marked cell's log-odds is read once and both planes written once
+//                           (the updateIndex plane is never read).  No global atomics; see DESIGN.md.
+// Wrong-result pricing builds (no atomics, no walk, no apply, hardware exp) are not in this file:
+// tools/build_diag.py derives them from a copy of the sources.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "detmath.h"
 #include "hector_internal.h"
-
-#ifndef S2D_MATCH_ABL
-#define S2D_MATCH_ABL 0  // diagnostic builds only: 1 hardware exp, 2 no cell gathers
-#endif
 
 namespace s2d {
 
@@ -72,11 +72,7 @@ __device__ __forceinline__ bool pose_diff_larger(const float *p1, const float *p
 // GridMapLogOddsFunctions::getGridProbability  H/map/GridMapLogOdds.h:136-140
 __device__ __forceinline__ float cell_prob(float l)
 {
-#if S2D_MATCH_ABL == 1
-    float odds = __expf(l);  // diagnostic only
-#else
     float odds = sdm_expf(l);
-#endif
     return __fdiv_rn(odds, odds + 1.0f);
 }
 
@@ -132,9 +128,6 @@ __device__ __forceinline__ void point_fetch(const float *__restrict__ lvl_words,
         pf.fx = x - (float)ix;
         pf.fy = y - (float)iy;
         // 4 neighbours (:160-192); ix <= sx-2, iy <= sy-2 by the bounds check
-#if S2D_MATCH_ABL == 2
-        pf.l[0] = (float)(ix & 7) * 0.01f; pf.l[1] = (float)(iy & 7) * 0.01f; pf.l[2] = 0.0f; pf.l[3] = 0.0f;
-#else
         const unsigned ux = (unsigned)ix, uy = (unsigned)iy;  // >= 0 by the bounds check
         const float *r0 = lvl_words + cell_word(g, (int)ux, (int)uy);
         const float *r1 = lvl_words + cell_word(g, (int)ux, (int)(uy + 1));
@@ -150,7 +143,6 @@ __device__ __forceinline__ void point_fetch(const float *__restrict__ lvl_words,
             pf.l[2] = r1[0];
             pf.l[3] = lvl_words[cell_word(g, (int)(ux + 1), (int)(uy + 1))];
         }
-#endif
     }
 }
 
@@ -478,8 +470,9 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     }
     st.clamp_count += clamps;
     st.tot_steps += 1;
-    if (plog.buf && s < plog.streams && st.step_index < plog.capacity) {
-        float *row = plog.buf + ((size_t)st.step_index * plog.streams + s) * 3;
+    const int slot = plog.slot_of ? plog.slot_of[s] : s;
+    if (plog.buf && slot >= 0 && slot < plog.streams && st.step_index < plog.capacity) {
+        float *row = plog.buf + ((size_t)st.step_index * plog.streams + slot) * 3;
         row[0] = np_[0];
         row[1] = np_[1];
         row[2] = np_[2];
@@ -1024,11 +1017,7 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
 #pragma unroll
             for (int row = 0; row < TILE_H; ++row) {
                 const int gy = Y0 + row;
-#ifdef S2D_ABL_NOLOAD
-                cl[row] = (float)row;
-#else
                 if (((rowmask >> row) & 1u) && colok && gy < g.sy) cl[row] = tl[row * TILE + lane];
-#endif
             }
             S2D_STAMP(tb);
             bool any = false;
@@ -1125,12 +1114,8 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
                         if (l < 50.0f) l = l + lo;  // updateSetOccupied (:108-114)
                         upd = mark_occ;
                     }
-#ifdef S2D_ABL_NOSTORE
-                    asm volatile("" ::"v"(l), "v"(upd));
-#else
                     tl[row * TILE + lane] = l;
                     tu[row * TILE + lane] = upd;
-#endif
                     ++touched;
                 }
 #pragma unroll
@@ -1180,9 +1165,6 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
 #ifndef S2D_UPD_STRIDE
 #define S2D_UPD_STRIDE 68
 #endif
-#ifndef S2D_APPLY_UPD_LOAD
-#define S2D_APPLY_UPD_LOAD 1  // 1: updateIndex quads loaded + stored whole; 0: per-cell masked stores
-#endif
 constexpr int UPD_STRIDE = S2D_UPD_STRIDE;            // LDS words per tile row (16-B rows, no 64-stride conflicts)
 #ifndef S2D_UPD_TH
 #define S2D_UPD_TH 32
@@ -1202,22 +1184,18 @@ constexpr int UPD_QUADS = TILE * UPD_TH / 4 / UPD_THREADS;  // apply quads per t
 // order updateByScan walks the beams).  A beam never frees its own end cell, so with the hit bit
 // set an odd word means a lower-index beam freed the cell before the first beam that hits it, an
 // even word that the hit came first -- all that bresenhamCellFree / bresenhamCellOcc (:302-330)
-// depend on within one scan.  GridMapLogOddsFunctions (GridMapLogOdds.h:108-129):
-__device__ __forceinline__ int apply_cell(float &l, int &u, unsigned m, unsigned hit, float lf, float lo, int mf, int mo)
+// depend on within one scan.  A quad's marks are carried in registers as 12 bits: bit c "marked",
+// bit 4 + c "odd event word", bit 8 + c "hit" for its cells c = 0..3.
+// GridMapLogOddsFunctions (GridMapLogOdds.h:108-129) applied to one marked cell:
+__device__ __forceinline__ float apply_cell(float l, unsigned odd, unsigned hit, float lf, float lo)
 {
-    if (m == W_NONE) return 0;
-    if (!hit) {
-        l = l + lf;        // updateSetFree (:120-124)
-        u = mf;
-    } else {
-        if (m & 1u) {
-            l = l + lf;    // bresenhamCellFree by an earlier beam
-            l = l - lf;    // updateUnsetFree (:126-129)
-        }
-        if (l < 50.0f) l = l + lo;  // updateSetOccupied (:108-114)
-        u = mo;
+    if (!hit) return l + lf;   // updateSetFree (:120-124)
+    if (odd) {
+        l = l + lf;            // bresenhamCellFree by an earlier beam
+        l = l - lf;            // updateUnsetFree (:126-129)
     }
-    return 1;
+    if (l < 50.0f) l = l + lo; // updateSetOccupied (:108-114)
+    return l;
 }
 
 // word offset of LDS-tile row `row` inside the level's tiled storage, relative to the LDS tile's
@@ -1231,18 +1209,10 @@ __device__ __forceinline__ int upd_off(int row, int tiles_x)
 constexpr int UPD_HIT_WORDS = UPD_TH * (TILE / 32);                  // one hit bit per tile cell
 constexpr int UPD_MARK_WORDS = (UPD_TILE_WORDS + UPD_HIT_WORDS + 3) & ~3;
 
-constexpr int UPD_FIXED_WORDS = UPD_MARK_WORDS;  // + rays + fan-group boxes (per scan size)
+constexpr int UPD_FIXED_WORDS = 2 * UPD_MARK_WORDS + 4;  // two mark buffers + flags; + rays + fan-group boxes
 
-// the free mark of one raster step: blind LDS atomicMin of the event code (S2D_DIAG_PLAIN: a plain
-// store -- wrong results, a diagnostic build that prices the atomic)
-__device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev)
-{
-#ifdef S2D_DIAG_PLAIN
-    *reinterpret_cast<volatile unsigned *>(p) = ev;
-#else
-    atomicMin(p, ev);
-#endif
-}
+// the free mark of one raster step: blind LDS atomicMin of the event code
+__device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) { atomicMin(p, ev); }
 
 __device__ __forceinline__ int lane_rank(unsigned long long m)  // set lanes below this one
 {
@@ -1265,6 +1235,7 @@ __device__ __forceinline__ int fan_beam(int b0, int lane)  // b0 = 256 G + 64 w
 #endif
 }
 __host__ __device__ constexpr int fan_groups(int max_points) { return ((max_points + 255) / 256) * 4; }
+constexpr int UPD_GROUP_WORDS = 4;  // LDS words per fan group: its bounding box
 
 // Grid: for level l, upd_parts[l] x count blocks (level-major, then part, then stream); part p of a
 // level draws the tiles t = p, p + parts, ... of the scan's tile box (t row-major over the box).
@@ -1274,9 +1245,10 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                  const UpdList *__restrict__ wl, UpdList *__restrict__ wl_next, int ncu)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned smem[];
-    unsigned *marks = smem;                            // UPD_TILE_WORDS event words
-    unsigned *hitb = smem + UPD_TILE_WORDS;            // UPD_HIT_WORDS hit bits
-    unsigned *rays = smem + UPD_MARK_WORDS;            // max_points packed end cells
+    // two mark buffers (tile i rasters into buffer i & 1 while tile i - 1's cells are applied),
+    // each UPD_TILE_WORDS event words + UPD_HIT_WORDS hit bits; then 4 flag words, rays, fan boxes
+    volatile unsigned *s_any = smem + 2 * UPD_MARK_WORDS;   // [2] "tile has a mark" per buffer
+    unsigned *rays = smem + UPD_FIXED_WORDS;               // max_points packed end cells
     int4 *gbox = reinterpret_cast<int4 *>(rays + ((max_points + 3) & ~3));  // per fan group: x0 y0 x1 y1
     const int lane = threadIdx.x & 63;
     __shared__ int s_bbox[4];
@@ -1309,10 +1281,6 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     const int tid = threadIdx.x;
     float *lvw = cells + (size_t)s * geom.stream_words + g.word_offset;
 
-#ifdef S2D_STAMPS
-    unsigned long long t_a = 0, t_b = 0, t_c = 0, t_d = 0, c_setup = 0, c_raster = 0, c_apply = 0, n_tiles = 0;
-    S2D_STAMP(t_a);
-#endif
     const RayFrame fr = ray_frame(g, st);
     const int x0 = fr.bxi, y0 = fr.byi;
     if (tid == 0) {
@@ -1370,190 +1338,158 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     unsigned touched = 0;
 
     const int ntx = tx1 - tx0 + 1, ntiles = ntx * (ty1 - ty0 + 1);
-#ifdef S2D_STAMPS
-    S2D_STAMP(t_b);
-    c_setup = t_b - t_a;
-#endif
-    for (int t = part; t < ntiles; t += parts) {
+    const int my_tiles = ntiles > part ? (ntiles - part + parts - 1) / parts : 0;
+    // Two-stage pipeline over this workgroup's tiles t_i = part + i * parts:
+    //   iteration i: clear buffer i & 1 -> barrier -> raster tile i -> apply tile i - 1 from registers
+    //   (its cell loads were issued one raster earlier) -> barrier -> read tile i's marks into
+    //   registers and issue the loads of its marked quads.
+    // The barriers only wait for LDS traffic (lds_barrier), so the loads and the previous tile's stores
+    // stay in flight across them.  A buffer is cleared two iterations after its marks were read, with
+    // both barriers of the iteration between.
+    float4 ql[UPD_QUADS];      // pending tile: log-odds of the marked quads (loads in flight)
+    unsigned qb[UPD_QUADS];    // pending tile: 12 mark bits per quad (see apply_cell)
+    float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)
+    for (int i = 0; i <= my_tiles; ++i) {
+        const int buf = i & 1;
+        unsigned *marks = smem + buf * UPD_MARK_WORDS;
+        unsigned *hitb = marks + UPD_TILE_WORDS;
+        const int t = part + i * parts;
         const int ty = ty0 + t / ntx, tx = tx0 + t % ntx;
         const int X0 = tx * TILE, Y0 = ty * UPD_TH;
         const int X1 = X0 + TILE, Y1 = Y0 + UPD_TH;
-        for (int k = tid; k < UPD_MARK_WORDS / 4; k += UPD_THREADS)
-            reinterpret_cast<uint4 *>(smem)[k] = k < UPD_TILE_WORDS / 4 ? make_uint4(W_NONE, W_NONE, W_NONE, W_NONE)
-                                                                        : make_uint4(0u, 0u, 0u, 0u);
-        __syncthreads();
-        bool any = false;
-        for (int b0 = tid & ~63; (b0 & ~255) < n; b0 += UPD_THREADS) {
-            // wave-uniform fan-group test (scalar)
-            const int4 gb = gbox[b0 >> 6];
-            const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
-            const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
-            if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
-            const int b = fan_beam(b0, lane);
-            const unsigned r = b < n ? rays[b] : RAY_INVALID;
-            int scnt = 0;           // free steps of this beam inside the tile
-            RayWalk w = {};
-            int lo_i = 0, q = 0, err = 0;
-            if (r != RAY_INVALID) {
-                const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-                if (!(max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1)) {
-                    if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {  // bresenhamCellOcc (:266)
-                        const int c = (y1 - Y0) * TILE + (x1 - X0);
-                        atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
-                        atomicOr(&hitb[c >> 5], 1u << (c & 31));
-                        any = true;
-                    }
-                    w = ray_walk(x0, y0, x1, y1);
-                    int hi_i;
-                    const bool in = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i)
-                                              : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
-                    if (in) {
-                        if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
-                        if (lo_i <= hi_i) {
-                            scnt = hi_i - lo_i + 1;
-                            const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
-                            q = (int)udiv_small(num, (unsigned)w.da);
-                            err = (int)(num - (unsigned)q * (unsigned)w.da);
+        if (i < my_tiles) {
+            for (int k = tid; k < UPD_MARK_WORDS / 4; k += UPD_THREADS)
+                reinterpret_cast<uint4 *>(marks)[k] = k < UPD_TILE_WORDS / 4 ? make_uint4(W_NONE, W_NONE, W_NONE, W_NONE)
+                                                                            : make_uint4(0u, 0u, 0u, 0u);
+            if (tid == 0) s_any[buf] = 0u;
+            lds_barrier();
+            bool any = false;
+            for (int b0 = tid & ~63; (b0 & ~255) < n; b0 += UPD_THREADS) {
+                // wave-uniform fan-group test (scalar)
+                const int4 gb = gbox[b0 >> 6];
+                const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
+                const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
+                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
+                const int b = fan_beam(b0, lane);
+                const unsigned r = b < n ? rays[b] : RAY_INVALID;
+                int scnt = 0;           // free steps of this beam inside the tile
+                RayWalk w = {};
+                int lo_i = 0, q = 0, err = 0;
+                if (r != RAY_INVALID) {
+                    const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+                    if (!(max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1)) {
+                        if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {  // bresenhamCellOcc (:266)
+                            const int c = (y1 - Y0) * TILE + (x1 - X0);
+                            atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
+                            atomicOr(&hitb[c >> 5], 1u << (c & 31));
                             any = true;
+                        }
+                        w = ray_walk(x0, y0, x1, y1);
+                        int hi_i;
+                        const bool in = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i)
+                                                  : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
+                        if (in) {
+                            if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
+                            if (lo_i <= hi_i) {
+                                scnt = hi_i - lo_i + 1;
+                                const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
+                                q = (int)udiv_small(num, (unsigned)w.da);
+                                err = (int)(num - (unsigned)q * (unsigned)w.da);
+                                any = true;
+                            }
                         }
                     }
                 }
-            }
-            const unsigned ev = 2u * (unsigned)b + 1u;
-            // LDS index of step lo_i and its increments along the major / minor axis
-            const int la = w.x_major ? 1 : UPD_STRIDE;
-            const int lb = w.x_major ? UPD_STRIDE : 1;
-            const int ax = w.a0 + w.sa * lo_i - (w.x_major ? X0 : Y0);
-            const int bx = w.b0 + w.sb * q - (w.x_major ? Y0 : X0);
-            const int li = ax * la + bx * lb;
-            const int da_step = w.sa * la, db_step = w.sb * lb;
-#ifdef S2D_VISITS
-            {
-                const unsigned long long am = __ballot(scnt > 0);
-                int mx = scnt, sm = scnt;
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) {
-                    mx = max(mx, __shfl_xor(mx, off, 64));
-                    sm += __shfl_xor(sm, off, 64);
+                if (scnt <= 0) continue;
+                const unsigned ev = 2u * (unsigned)b + 1u;
+                // LDS index of step lo_i and its increments along the major / minor axis
+                const int la = w.x_major ? 1 : UPD_STRIDE;
+                const int lb = w.x_major ? UPD_STRIDE : 1;
+                const int ax = w.a0 + w.sa * lo_i - (w.x_major ? X0 : Y0);
+                const int bx = w.b0 + w.sb * q - (w.x_major ? Y0 : X0);
+                const int li = ax * la + bx * lb;
+                // incremental walk, f = da - 1 - error_b: the minor axis steps when f - db < 0; byte
+                // offsets into the mark array, two steps per trip
+                const int dab = w.sa * la * 4, dbb = w.sb * lb * 4;
+                const int da_ = w.da, db_ = w.db;
+                int f = da_ - 1 - err;
+                char *pm = reinterpret_cast<char *>(marks) + li * 4;
+                int k = 0;
+                for (; k + 1 < scnt; k += 2) {
+                    upd_mark(reinterpret_cast<unsigned *>(pm), ev);  // bresenhamCellFree (:302-312)
+                    int g2 = f - db_;
+                    int m = g2 >> 31;
+                    f = g2 + (m & da_);
+                    pm += dab + (m & dbb);
+                    upd_mark(reinterpret_cast<unsigned *>(pm), ev);
+                    g2 = f - db_;
+                    m = g2 >> 31;
+                    f = g2 + (m & da_);
+                    pm += dab + (m & dbb);
                 }
-                if (lane == 0) {
-                    atomicAdd(&g_stamps[4], 1ull);
-                    atomicAdd(&g_stamps[5], (unsigned long long)__popcll(am));
-                    atomicAdd(&g_stamps[6], (unsigned long long)sm);
-                    atomicAdd(&g_stamps[7], (unsigned long long)mx);
+                if (k < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
+            }
+            if (__ballot(any) && lane == 0) s_any[buf] = 1u;
+        }
+        if (pend_tl) {
+            // apply the previous tile: log-odds of every marked cell, both planes written per marked
+            // cell (whole 16-B stores for fully marked quads); the updateIndex plane is never read --
+            // a cell's stored index always predates this scan's marks (currUpdateIndex += 3 per scan)
+            int *tu = reinterpret_cast<int *>(pend_tl + TILE_CELLS);
+#pragma unroll
+            for (int j = 0; j < UPD_QUADS; ++j) {
+                const unsigned mb = qb[j];
+                if (!(mb & 15u)) continue;
+                const int qi = tid + j * UPD_THREADS;
+                const int o = upd_off(qi >> 4, g.tiles_x) + ((qi & 15) << 2);
+                float4 v = ql[j];
+                const float lv[4] = {v.x, v.y, v.z, v.w};
+                float nv[4];
+                int uv[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    nv[c] = apply_cell(lv[c], (mb >> (4 + c)) & 1u, (mb >> (8 + c)) & 1u, lf, lo);
+                    uv[c] = ((mb >> (8 + c)) & 1u) ? mark_occ : mark_free;
+                }
+                if ((mb & 15u) == 15u) {
+                    *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);
+                    *reinterpret_cast<int4 *>(&tu[o]) = make_int4(uv[0], uv[1], uv[2], uv[3]);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        if ((mb >> c) & 1u) {
+                            pend_tl[o + c] = nv[c];
+                            tu[o + c] = uv[c];
+                        }
+                }
+                touched += __popc(mb & 15u);
+            }
+            pend_tl = nullptr;
+        }
+        if (i < my_tiles) {
+            lds_barrier();  // tile i's marks complete
+            if (s_any[buf]) {
+                // thread owns quads q = tid + j * 256 (16 quads per 64-cell row); cells outside the map
+                // (padding of edge tiles) never carry marks
+                pend_tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
+#pragma unroll
+                for (int j = 0; j < UPD_QUADS; ++j) {
+                    const int qi = tid + j * UPD_THREADS;
+                    const int row = qi >> 4, c4 = (qi & 15) << 2;
+                    const uint4 m = *reinterpret_cast<const uint4 *>(&marks[row * UPD_STRIDE + c4]);
+                    const unsigned h = (hitb[row * (TILE / 32) + (c4 >> 5)] >> (c4 & 31)) & 15u;
+                    const unsigned mk = (unsigned)(m.x != W_NONE) | ((unsigned)(m.y != W_NONE) << 1) |
+                                        ((unsigned)(m.z != W_NONE) << 2) | ((unsigned)(m.w != W_NONE) << 3);
+                    const unsigned od = (m.x & 1u) | ((m.y & 1u) << 1) | ((m.z & 1u) << 2) | ((m.w & 1u) << 3);
+                    qb[j] = mk | ((od & mk) << 4) | ((h & mk) << 8);
+                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(&pend_tl[upd_off(row, g.tiles_x) + c4]);
                 }
             }
-#endif
-#ifdef S2D_DIAG_NOSTEP
-            continue;  // diagnostic build only: group setup cost without the walk
-#endif
-            if (scnt <= 0) continue;
-            // incremental walk, f = da - 1 - error_b: the minor axis steps when f - db < 0; byte
-            // offsets into the mark array, two steps per trip
-            const int dab = da_step * 4, dbb = db_step * 4;
-            const int da_ = w.da, db_ = w.db;
-            int f = da_ - 1 - err;
-            char *pm = reinterpret_cast<char *>(marks) + li * 4;
-            int i = 0;
-            for (; i + 1 < scnt; i += 2) {
-                upd_mark(reinterpret_cast<unsigned *>(pm), ev);  // bresenhamCellFree (:302-312)
-                int g2 = f - db_;
-                int m = g2 >> 31;
-                f = g2 + (m & da_);
-                pm += dab + (m & dbb);
-                upd_mark(reinterpret_cast<unsigned *>(pm), ev);
-                g2 = f - db_;
-                m = g2 >> 31;
-                f = g2 + (m & da_);
-                pm += dab + (m & dbb);
-            }
-            if (i < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
         }
-        const bool tile_any = __syncthreads_or(any);
-#ifdef S2D_STAMPS
-        S2D_STAMP(t_c);
-        c_raster += t_c - t_b;
-        t_b = t_c;
-#endif
-        if (!tile_any) continue;
-#ifdef S2D_DIAG_NOAPPLY
-        __syncthreads();
-        continue;  // diagnostic build only: the tile's apply phase skipped
-#endif
-        // apply: thread owns quads q = tid + j * 256 (16 quads per 64-cell row): 16-B LDS reads of the
-        // event words, 16-B global loads / stores of both planes for every quad holding a mark.  Cells
-        // outside the map (padding of edge tiles) never carry marks and are rewritten unchanged.
-        // quad qi: LDS row qi / 16, storage tile (tx, (Y0 + row) / TILE_H), storage row (Y0 + row) % TILE_H
-        float *tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
-        int *tu = reinterpret_cast<int *>(tl + TILE_CELLS);
-        uint4 qm[UPD_QUADS];
-        unsigned qh[UPD_QUADS];
-        float4 ql[UPD_QUADS];
-        int4 qu[UPD_QUADS];
-        bool qa[UPD_QUADS];
-#pragma unroll
-        for (int j = 0; j < UPD_QUADS; ++j) {
-            const int qi = tid + j * UPD_THREADS;
-            const int row = qi >> 4, c4 = (qi & 15) << 2;
-            qm[j] = *reinterpret_cast<const uint4 *>(&marks[row * UPD_STRIDE + c4]);
-            qh[j] = hitb[row * (TILE / 32) + (c4 >> 5)] >> (c4 & 31);
-            qa[j] = (qm[j].x & qm[j].y & qm[j].z & qm[j].w) != W_NONE;
-            if (qa[j]) {
-                ql[j] = *reinterpret_cast<const float4 *>(&tl[upd_off(row, g.tiles_x) + c4]);
-#if S2D_APPLY_UPD_LOAD
-                qu[j] = *reinterpret_cast<const int4 *>(&tu[upd_off(row, g.tiles_x) + c4]);
-#endif
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < UPD_QUADS; ++j) {
-            if (!qa[j]) continue;
-            const int qi = tid + j * UPD_THREADS;
-            const int row = qi >> 4, c4 = (qi & 15) << 2;
-#if S2D_APPLY_UPD_LOAD
-            touched += apply_cell(ql[j].x, qu[j].x, qm[j].x, qh[j] & 1u, lf, lo, mark_free, mark_occ);
-            touched += apply_cell(ql[j].y, qu[j].y, qm[j].y, qh[j] & 2u, lf, lo, mark_free, mark_occ);
-            touched += apply_cell(ql[j].z, qu[j].z, qm[j].z, qh[j] & 4u, lf, lo, mark_free, mark_occ);
-            touched += apply_cell(ql[j].w, qu[j].w, qm[j].w, qh[j] & 8u, lf, lo, mark_free, mark_occ);
-            *reinterpret_cast<float4 *>(&tl[upd_off(row, g.tiles_x) + c4]) = ql[j];
-            *reinterpret_cast<int4 *>(&tu[upd_off(row, g.tiles_x) + c4]) = qu[j];
-#else
-            int u[4];
-            const int t0 = apply_cell(ql[j].x, u[0], qm[j].x, qh[j] & 1u, lf, lo, mark_free, mark_occ);
-            const int t1 = apply_cell(ql[j].y, u[1], qm[j].y, qh[j] & 2u, lf, lo, mark_free, mark_occ);
-            const int t2 = apply_cell(ql[j].z, u[2], qm[j].z, qh[j] & 4u, lf, lo, mark_free, mark_occ);
-            const int t3 = apply_cell(ql[j].w, u[3], qm[j].w, qh[j] & 8u, lf, lo, mark_free, mark_occ);
-            touched += t0 + t1 + t2 + t3;
-            const int o = upd_off(row, g.tiles_x) + c4;
-            *reinterpret_cast<float4 *>(&tl[o]) = ql[j];
-            if (t0) tu[o + 0] = u[0];
-            if (t1) tu[o + 1] = u[1];
-            if (t2) tu[o + 2] = u[2];
-            if (t3) tu[o + 3] = u[3];
-#endif
-        }
-        __syncthreads();
-#ifdef S2D_STAMPS
-        S2D_STAMP(t_d);
-        c_apply += t_d - t_b;
-        t_b = t_d;
-        ++n_tiles;
-#endif
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);
     if (lane == 0 && touched) atomicAdd(&state[s].tot_touched, (unsigned long long)touched);
-#ifdef S2D_STAMPS
-#ifdef S2D_STAMPS_LVL
-    if (lvl != S2D_STAMPS_LVL) return;
-#endif
-    if (tid == 0) {
-        atomicAdd(&g_stamps[0], c_setup);
-        atomicAdd(&g_stamps[1], c_raster);
-        atomicAdd(&g_stamps[2], c_apply);
-        atomicAdd(&g_stamps[3], n_tiles);
-    }
-#endif
 }
 
 // --------------------------------------------------------------------------- utility kernels

@@ -368,16 +368,20 @@ int kt_create(kt_ctx **out, const kt_laser *laser, const kt_params *params, int 
                     !(bpm && (!strcmp(bpm, "per_base") || !strcmp(bpm, "cas")));
     }
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamDefault)) != hipSuccess) {
         delete c;
         return kfail(KT_EHIP, "hipStreamCreate", e);
     }
     const size_t S = (size_t)max_scans, n = (size_t)g.n, M = (size_t)c->slots;
     const size_t mp = (size_t)g.max_poses, npos = (size_t)g.nxy * g.nxy;
-#define KALLOC(ptr, bytes)                                             \
-    if ((e = hipMalloc((void **)&(ptr), (bytes))) != hipSuccess) {     \
-        kt_destroy(c);                                                 \
-        return kfail(KT_ENOMEM, "hipMalloc " #ptr, e);                 \
+    // SLAM2D_POISON=1 (test hook): fill every buffer with 0xA5 bytes first, so that a kernel reading
+    // memory the context never initialised fails its parity test instead of passing on fresh zero pages
+    const bool poison = getenv("SLAM2D_POISON") && atoi(getenv("SLAM2D_POISON")) != 0;
+#define KALLOC(ptr, bytes)                                                                  \
+    if ((e = hipMalloc((void **)&(ptr), (bytes))) != hipSuccess ||                          \
+        (poison && (e = hipMemsetAsync((ptr), 0xA5, (bytes), c->stream)) != hipSuccess)) {  \
+        kt_destroy(c);                                                                      \
+        return kfail(KT_ENOMEM, "hipMalloc " #ptr, e);                                      \
     }
     KALLOC(c->d_ranges, sizeof(double) * S * n);
     KALLOC(c->d_poses, sizeof(double) * S * 3);

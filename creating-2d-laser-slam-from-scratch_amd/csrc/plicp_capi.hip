@@ -82,7 +82,7 @@ int pl_create(pl_ctx **out, int max_pairs, int max_rays, const pl_params *params
     if (params) c->params = *params;
     else pl_default_params(&c->params);
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamDefault)) != hipSuccess) {
         delete c;
         return pfail(PL_EHIP, "hipStreamCreate", e);
     }

@@ -55,6 +55,8 @@ def _declare(L):
     L.hs_get_queue_stats.argtypes = [_p, _p, _i]
     L.hs_get_device_buffers.argtypes = [_p, P(_p), P(C.c_size_t), P(C.c_size_t)]
     L.hs_set_pose_log.argtypes = [_p, _p, _i, _i]
+    L.hs_set_pose_log_slots.argtypes = [_p, _p, _p, _i, _i]
+    L.hs_run_ranges_device.argtypes = [_p, _i, _p, _i, C.c_size_t, _p]
     L.hs_get_stream.restype = _p
     L.hs_get_stream.argtypes = [_p]
     L.hs_set_timing.argtypes = [_p, _i]

@@ -235,6 +235,12 @@ class HectorFleet:
                                                  C.c_void_p(d_hints or None), C.c_void_p(hip_stream or None)),
               "hs_step_ranges_batch_device")
 
+    def run_ranges_device(self, steps: int, d_ranges: int, range_stride: int, step_stride: int, hip_stream: int = 0):
+        """scanCallback for `steps` consecutive scans of every stream (step k at d_ranges + k * step_stride
+        floats); two fleet halves pipelined on two HIP streams, joined on hip_stream."""
+        check(self.L.hs_run_ranges_device(self.h, int(steps), C.c_void_p(d_ranges), int(range_stride),
+                                          int(step_stride), C.c_void_p(hip_stream or None)), "hs_run_ranges_device")
+
     def update_ranges(self, stream: int, ranges):
         """scanCallback for one stream from host ranges (float32 [n_beams])."""
         r = np.ascontiguousarray(ranges, np.float32)
@@ -261,6 +267,11 @@ class HectorFleet:
     def set_pose_log(self, d_buf: int, streams: int, capacity: int):
         """Device pose log (float32 [capacity][streams][3]) filled by every step; d_buf = 0 disables."""
         check(self.L.hs_set_pose_log(self.h, C.c_void_p(d_buf or None), int(streams), int(capacity)), "hs_set_pose_log")
+
+    def set_pose_log_slots(self, d_buf: int, d_slot_of_stream: int, slots: int, capacity: int):
+        """Device pose log of any subset of streams: stream s -> slot d_slot_of_stream[s] (< 0: not logged)."""
+        check(self.L.hs_set_pose_log_slots(self.h, C.c_void_p(d_buf or None), C.c_void_p(d_slot_of_stream or None),
+                                           int(slots), int(capacity)), "hs_set_pose_log_slots")
 
     def queue_stats(self, reset_stamps=True):
         o = np.zeros(8, np.int64)

@@ -14,11 +14,15 @@
  *     No exceptions cross the boundary.  The reference itself has no error reporting; its silent
  *     semantics are kept (empty scan -> hint, out-of-map beam -> skipped, singular H -> no step).
  *   - a context holds `num_streams` independent SLAM streams (one map pyramid each) resident in HBM.
- *     num_streams = 1 is the ROS drop-in; > 1 is the batched throughput path.  A context is not
- *     thread-safe: serialise calls (the reference serialises on the ROS spin thread).
+ *     num_streams = 1 is the ROS drop-in; > 1 is the batched throughput path.  Calls on one context
+ *     may come from several host threads (e.g. the publish thread's hs_get_map beside the spin
+ *     thread's hs_update, hector_slam.cc:201 / :277): an internal mutex serialises them.
  *   - host-pointer entry points copy through pinned staging and synchronise; *_device entry points
- *     take device pointers and a hipStream_t (as void*, NULL = the context's own stream) and do not
- *     synchronise.
+ *     take device pointers and a hipStream_t (as void*, NULL = the context's own stream, a blocking
+ *     stream, so it is ordered after work queued on the legacy default stream) and do not
+ *     synchronise.  Device work of one context is ordered across streams: every call first waits
+ *     (on its own stream) for the context's previous device work, so consecutive calls may use
+ *     different HIP streams.
  */
 #ifndef SLAM2D_HECTOR_H
 #define SLAM2D_HECTOR_H
@@ -131,6 +135,14 @@ int hs_ingest_batch_device(hs_ctx *ctx, int count, const float *d_ranges, int ra
  * one HectorSlamProcessor::update per stream (as hs_step_batch_device; hints NULL = last pose). */
 int hs_step_ranges_batch_device(hs_ctx *ctx, int stream_begin, int count, const float *d_ranges, int range_stride,
                                 const float *d_hints, void *hip_stream);
+/* scanCallback for `steps` consecutive scans of EVERY stream (offline / bag replay of a whole fleet):
+ * step k's ranges start at d_ranges + k * step_stride floats, stream s's at + s * range_stride.  Equal,
+ * bit for bit, to `steps` calls of hs_step_ranges_batch_device(ctx, 0, num_streams, ...) with NULL hints
+ * (the streams are independent).  With SLAM2D_PIPELINE=1 in the environment at hs_create, the fleet runs
+ * as two halves on two HIP streams so that one half's grid update overlaps the other half's match
+ * (measured slower on MI355X at 1024 streams).  hip_stream waits for all of it. */
+int hs_run_ranges_device(hs_ctx *ctx, int steps, const float *d_ranges, int range_stride, size_t step_stride,
+                         void *hip_stream);
 /* scanCallback for one stream from host ranges (the ROS drop-in entry point). */
 int hs_update_ranges(hs_ctx *ctx, int stream, const float *ranges, float pose_out[3], float cov_out[9],
                      int *did_update_out);
@@ -156,6 +168,9 @@ int hs_get_device_buffers(hs_ctx *ctx, void **cells, size_t *cells_bytes, size_t
  * at row = steps since hs_reset, i.e. d_buf[(row*streams + s)*3]; rows >= capacity are dropped.
  * d_buf NULL disables.  The caller owns d_buf (device memory of >= capacity*streams*3 floats). */
 int hs_set_pose_log(hs_ctx *ctx, float *d_buf, int streams, int capacity);
+/* The same for any subset of streams: stream s is logged in slot d_slot_of_stream[s] (device int[num_streams],
+ * < 0 = not logged), i.e. d_buf[(row*slots + slot)*3]. */
+int hs_set_pose_log_slots(hs_ctx *ctx, float *d_buf, const int *d_slot_of_stream, int slots, int capacity);
 /* The context's own HIP stream (hipStream_t as void*). */
 void *hs_get_stream(hs_ctx *ctx);
 

@@ -165,3 +165,90 @@ def test_update_ranges_host_entry_equals_batch(gpu):
         b.step_ranges_device(d_r.data_ptr(), N)
         pb = b.poses()[0][0]
         assert np.array_equal(_bits(pa), _bits(pb)), t
+
+
+def _maps_equal(fa, fb, S, LV):
+    for s in range(S):
+        for lvl in range(LV):
+            ma, mb = fa.get_map(s, lvl), fb.get_map(s, lvl)
+            assert np.array_equal(ma["upd"], mb["upd"]), (s, lvl)
+            assert np.array_equal(_bits(ma["logodds"]), _bits(mb["logodds"])), (s, lvl)
+
+
+@pytest.mark.parametrize("S,gate,pipeline", [(7, (-1.0, -1.0), "1"), (6, (0.4, 0.9), "1"), (1, (-1.0, -1.0), "1"),
+                                             (5, (0.4, 0.9), "0")])
+def test_run_ranges_equals_per_step(gpu, monkeypatch, S, gate, pipeline):
+    """hs_run_ranges_device (K steps in one call; SLAM2D_PIPELINE=1: two fleet halves on two HIP streams,
+    the grid update of one half beside the other half's match) == K calls of
+    hs_step_ranges_batch_device, every pose, gate, map cell and pose-log entry bit for bit; odd fleets
+    split unevenly, S = 1 runs unsplit.  Stream S-1 is also replayed on the oracle."""
+    import torch
+    T, LV, SIZE = 8, 2, 384
+    scans = synth.make_streams(S, T, with_points=False, seed=77)
+    L = _roll_pi_laser()
+    monkeypatch.setenv("SLAM2D_PIPELINE", pipeline)
+    fa = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
+    monkeypatch.delenv("SLAM2D_PIPELINE")
+    fb = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
+    logs = []
+    for f in (fa, fb):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(*gate)
+        f.set_laser(L)
+        d_log = torch.zeros((T, S, 3), dtype=torch.float32, device="cuda")
+        f.set_pose_log(d_log.data_ptr(), S, T)
+        logs.append(d_log)
+    r = np.ascontiguousarray(scans.ranges.transpose(1, 0, 2))      # [T][S][N]
+    d_r = torch.from_numpy(r).cuda()
+    hs = torch.cuda.current_stream().cuda_stream   # the pose logs were zeroed on torch's stream
+    fa.run_ranges_device(T, d_r.data_ptr(), N, S * N, hip_stream=hs)
+    for t in range(T):
+        fb.step_ranges_device(d_r[t].data_ptr(), N, hip_stream=hs)
+    torch.cuda.synchronize()
+    pa, ca, da, _ = fa.poses()
+    pb, cb, db, _ = fb.poses()
+    assert np.array_equal(_bits(pa), _bits(pb)) and np.array_equal(_bits(ca), _bits(cb))
+    assert np.array_equal(da, db)
+    assert np.array_equal(_bits(logs[0].cpu().numpy()), _bits(logs[1].cpu().numpy()))
+    _maps_equal(fa, fb, S, LV)
+    o = O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=256)
+    o.set_update_factors(0.4, 0.9)
+    o.set_thresholds(*gate)
+    cs = O.unit_vectors(N, float(AMIN), float(AINC))
+    scale = fa.scale_to_map()
+    lg = logs[0].cpu().numpy()
+    for t in range(T):
+        pts, org = O.ingest(r[t, S - 1], cs, L.as_oracle_dict(), scale)
+        op, _, _ = o.process(pts, origo=tuple(org))
+        assert np.array_equal(_bits(lg[t, S - 1]), _bits(op)), t
+
+
+def test_device_calls_alternating_hip_streams(gpu):
+    """Consecutive *_device calls on one context issued on two different HIP streams (the context's
+    scratch -- update lists, ingest buffers -- is shared): each call waits for the previous one, so the
+    result equals issuing all calls on one stream."""
+    import torch
+    S, T, LV, SIZE = 16, 6, 2, 256
+    scans = synth.make_streams(S, T, with_points=False, seed=5)
+    L = _roll_pi_laser()
+    fa = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
+    fb = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
+    for f in (fa, fb):
+        f.set_thresholds(-1.0, -1.0)
+        f.set_laser(L)
+    r = np.ascontiguousarray(scans.ranges.transpose(1, 0, 2))
+    d_r = torch.from_numpy(r).cuda()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for t in range(T):
+        half = S // 2
+        # two disjoint stream ranges per step on two HIP streams, then the next step on the other pair
+        fa.step_ranges_device(d_r[t].data_ptr(), N, stream_begin=0, count=half,
+                              hip_stream=(s1 if t % 2 == 0 else s2).cuda_stream)
+        fa.step_ranges_device(d_r[t, half:].data_ptr(), N, stream_begin=half, count=S - half,
+                              hip_stream=(s2 if t % 2 == 0 else s1).cuda_stream)
+        fb.step_ranges_device(d_r[t].data_ptr(), N)
+    torch.cuda.synchronize()
+    pa, _, da, _ = fa.poses()
+    pb, _, db, _ = fb.poses()
+    assert np.array_equal(_bits(pa), _bits(pb)) and np.array_equal(da, db)
+    _maps_equal(fa, fb, S, LV)

@@ -109,14 +109,14 @@ def test_batch_device_matches_single(gpu):
     sm = karto.ScanMatcher(lz, p, max_matches=M, max_scans=S + M, max_base=B)
     pr = torch.tensor(np.concatenate([R, R[B:]]), dtype=torch.float64, device="cuda")
     pp = torch.tensor(np.concatenate([T, Q[B:]]), dtype=torch.float64, device="cuda")
-    sm.set_scans_device(0, S + M, pr.data_ptr(), pp.data_ptr())
+    sm.set_scans_device(0, S + M, pr.data_ptr(), pp.data_ptr(), hip_stream=torch.cuda.current_stream().cuda_stream)
     counts = [B - (i % 3) for i in range(M)]
     beg = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
     idx = np.concatenate([np.arange(B + i - c, B + i) for i, c in enumerate(counts)]).astype(np.int32)
     q = np.arange(S, S + M, dtype=np.int32)
     dq, db, di = (torch.tensor(a, device="cuda") for a in (q, beg, idx))
     res = torch.zeros(M * C.sizeof(karto.KtResult), dtype=torch.uint8, device="cuda")
-    sm.match_batch_device(M, dq.data_ptr(), db.data_ptr(), di.data_ptr(), res.data_ptr())
+    sm.match_batch_device(M, dq.data_ptr(), db.data_ptr(), di.data_ptr(), res.data_ptr(), hip_stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     out = karto.results_from_bytes(res.cpu().numpy())
     for i in range(M):
@@ -152,12 +152,12 @@ def test_batch_device_loop_window(gpu):
     sm = karto.ScanMatcher(lz, p, max_matches=M, max_scans=M * (K + 1), max_base=K)
     pr = torch.tensor(np.concatenate([QR, CR.reshape(-1, synth.N_BEAMS)]), dtype=torch.float64, device="cuda")
     pp = torch.tensor(np.concatenate([qp, CP.reshape(-1, 3)]), dtype=torch.float64, device="cuda")
-    sm.set_scans_device(0, M * (K + 1), pr.data_ptr(), pp.data_ptr())
+    sm.set_scans_device(0, M * (K + 1), pr.data_ptr(), pp.data_ptr(), hip_stream=torch.cuda.current_stream().cuda_stream)
     q = torch.arange(M, dtype=torch.int32, device="cuda")
     beg = torch.arange(M + 1, dtype=torch.int32, device="cuda") * K
     idx = torch.arange(M, M + M * K, dtype=torch.int32, device="cuda")
     res = torch.zeros(M * C.sizeof(karto.KtResult), dtype=torch.uint8, device="cuda")
-    sm.match_batch_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), res.data_ptr(), False, False)
+    sm.match_batch_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), res.data_ptr(), False, False, hip_stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     out = karto.results_from_bytes(res.cpu().numpy())
     for i in range(0, M, 7):
@@ -196,18 +196,18 @@ def test_sharded_window_equals_unsharded(gpu, loop, nshards, penalize, refine, M
 
     def ctx():
         sm = karto.ScanMatcher(lz, p, max_matches=M, max_scans=M * (K + 1), max_base=K)
-        sm.set_scans_device(0, M * (K + 1), pr.data_ptr(), pp.data_ptr())
+        sm.set_scans_device(0, M * (K + 1), pr.data_ptr(), pp.data_ptr(), hip_stream=torch.cuda.current_stream().cuda_stream)
         return sm
 
     ref = ctx()
     r0 = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
-    ref.match_batch_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), r0.data_ptr(), penalize, refine)
+    ref.match_batch_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), r0.data_ptr(), penalize, refine, hip_stream=torch.cuda.current_stream().cuda_stream)
     shards = [ctx() for _ in range(nshards)]
     words = shards[0].exchange_words()
     xs = [torch.full((M, words), -1, dtype=torch.int64, device="cuda") for _ in range(nshards)]
     for k, sm in enumerate(shards):
         sm.match_sharded_begin_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), k, nshards, xs[k].data_ptr(),
-                                      penalize)
+                                      penalize, hip_stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert all(bool((x >= 0).all()) for x in xs), "every exchange word is written and non-negative"
     x = xs[0].clone()
@@ -216,7 +216,7 @@ def test_sharded_window_equals_unsharded(gpu, loop, nshards, penalize, refine, M
     outs = []
     for sm in shards:
         r = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
-        sm.match_sharded_end_device(M, beg.data_ptr(), idx.data_ptr(), x.data_ptr(), r.data_ptr(), penalize, refine)
+        sm.match_sharded_end_device(M, beg.data_ptr(), idx.data_ptr(), x.data_ptr(), r.data_ptr(), penalize, refine, hip_stream=torch.cuda.current_stream().cuda_stream)
         outs.append(r)
     torch.cuda.synchronize()
     want = r0.cpu().numpy()
@@ -227,7 +227,7 @@ def test_sharded_window_equals_unsharded(gpu, loop, nshards, penalize, refine, M
     _same((res["mean"][0], res["covariance"][0].reshape(3, 3), res["response"][0]), o)
     # a context reused after the sharded path: the grids were cleared
     r2 = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
-    shards[0].match_batch_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), r2.data_ptr(), penalize, refine)
+    shards[0].match_batch_device(M, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), r2.data_ptr(), penalize, refine, hip_stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert np.array_equal(r2.cpu().numpy(), want)
 
@@ -243,8 +243,8 @@ def test_sharded_rejects_expansion_and_bad_shard(gpu):
     beg = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
     idx = torch.ones(1, dtype=torch.int32, device="cuda")
     with pytest.raises(karto.Slam2dError):
-        sm.match_sharded_begin_device(1, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), 0, 2, x.data_ptr())
+        sm.match_sharded_begin_device(1, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), 0, 2, x.data_ptr(), hip_stream=torch.cuda.current_stream().cuda_stream)
     p.use_response_expansion = 0
     sm2 = karto.ScanMatcher(lz, p, max_matches=1, max_scans=2, max_base=1)
     with pytest.raises(karto.Slam2dError):
-        sm2.match_sharded_begin_device(1, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), 2, 2, x.data_ptr())
+        sm2.match_sharded_begin_device(1, q.data_ptr(), beg.data_ptr(), idx.data_ptr(), 2, 2, x.data_ptr(), hip_stream=torch.cuda.current_stream().cuda_stream)

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Build a pricing / A-B variant of the product library from a patched COPY of the sources.
+
+  python tools/build_diag.py <variant> [<variant> ...]     -> creating-2d-laser-slam-from-scratch_amd/lib/libslam2d_<variant>.so
+
+The product sources carry no wrong-result switches: every variant here is a textual patch applied to
+a temporary copy of csrc/ (the build fails loudly if a patch no longer applies).  Variants marked
+WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); never ship them.
+
+  plain      WRONG RESULTS  hs_update_kernel marks with plain LDS stores instead of atomicMin
+  noapply    WRONG RESULTS  hs_update_kernel skips the apply phase (no global loads / stores)
+  hwexp      WRONG RESULTS  hs_match_kernel uses the hardware exp instead of (float)exp(double)
+"""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "creating-2d-laser-slam-from-scratch_amd")
+K = "hector_kernels.hip"
+
+PATCHES = {
+    "plain": [(K, "__device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) { atomicMin(p, ev); }",
+               "__device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) "
+               "{ *reinterpret_cast<volatile unsigned *>(p) = ev; }")],
+    "noapply": [(K, "        if (pend_tl) {\n", "        if (pend_tl && false) {\n")],
+    "hwexp": [(K, "    float odds = sdm_expf(l);", "    float odds = __expf(l);")],
+}
+
+
+def build(variant: str) -> str:
+    if variant not in PATCHES:
+        raise SystemExit(f"unknown variant {variant!r}; known: {', '.join(sorted(PATCHES))}")
+    tmp = tempfile.mkdtemp()
+    try:
+        src = os.path.join(tmp, "creating-2d-laser-slam-from-scratch_amd", "csrc")
+        shutil.copytree(os.path.join(PKG, "csrc"), src)
+        shutil.copytree(os.path.join(REPO, "include"), os.path.join(tmp, "include"))
+        for fname, old, new in PATCHES[variant]:
+            p = os.path.join(src, fname)
+            text = open(p).read()
+            if text.count(old) != 1:
+                raise SystemExit(f"variant {variant}: patch anchor not found exactly once in {fname}: {old[:60]!r}")
+            open(p, "w").write(text.replace(old, new))
+        out = os.path.join(PKG, "lib", f"libslam2d_{variant}.so")
+        subprocess.check_call(["make", "-s", "-C", src, f"OUT={out}"])
+        return out
+    finally:
+        shutil.rmtree(tmp)
+
+
+if __name__ == "__main__":
+    for v in sys.argv[1:]:
+        print("built", build(v))

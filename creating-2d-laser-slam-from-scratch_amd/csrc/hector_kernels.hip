@@ -186,6 +186,33 @@ __device__ __forceinline__ void point_accum(const PointFetch &pf, float cs, floa
     acc[8] = acc[8] + gy * rot;
 }
 
+// The 64-lane xor butterfly of the Hessian terms, offsets 32, 16, 8, 4, 2, 1 (the oracle's
+// reduce_threads = 256 order).  Offsets 32 and 16 go through ds_bpermute; after them a lane's value
+// equals that of lanes i ^ 16, i ^ 32, so the xor-8 partner is also the lane 8 further round its
+// 16-lane row (DPP row_ror:8), after that the xor-4 partner the lane 4 further (row_ror:4), and the
+// xor-2 / xor-1 partners are quad permutations.  Every lane adds exactly the value its xor partner
+// holds, in the same operand order, so the sums are bit-identical to the __shfl_xor butterfly.
+template <int NV>
+__device__ __forceinline__ void wave_butterfly(float (&acc)[NV])
+{
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = acc[k] + __shfl_xor(acc[k], 32, 64);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = acc[k] + __shfl_xor(acc[k], 16, 64);
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+        acc[k] = acc[k] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc[k]), 0x128, 0xF, 0xF, false));
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+        acc[k] = acc[k] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc[k]), 0x124, 0xF, 0xF, false));
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+        acc[k] = acc[k] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc[k]), 0x4E, 0xF, 0xF, false));
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+        acc[k] = acc[k] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc[k]), 0xB1, 0xF, 0xF, false));
+}
+
 #ifndef S2D_MATCH_BATCH
 #define S2D_MATCH_BATCH 2
 #endif
@@ -218,12 +245,7 @@ __device__ __forceinline__ void gn_step(const float *__restrict__ cells, const L
         for (int j = 0; j < MATCH_BATCH; ++j)
             if (i0 + j * MATCH_THREADS < n) point_accum(pf[j], cs, sn, acc);
     }
-    // 64-lane xor butterfly, offsets 32..1
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) acc[k] = acc[k] + __shfl_xor(acc[k], off, 64);
-    }
+    wave_butterfly(acc);  // 64-lane xor butterfly, offsets 32..1
     const int wave = tid >> 6;
     if ((tid & 63) == 0) {
 #pragma unroll
@@ -268,10 +290,15 @@ __device__ __forceinline__ void gn_step(const float *__restrict__ cells, const L
 // 4 exp and the 4 divisions; only waves with a moved point pay a gather round.  Keys reset per level.
 constexpr unsigned NB_NONE = 0xFFFFFFFFu;
 
+// Misses are compacted per wave: a lane that gathered a moved point's 4 log-odds parks them in the
+// point's cache slot and appends the slot to its wave's list; the wave then converts the listed slots
+// 64 at a time (4 exp + 4 divisions each) -- with per-slot branches the whole wave would pay the
+// conversion of slot j whenever ANY of its 64 lanes missed there, i.e. on nearly every step.
 template <int NP>
 __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
                                             int n, float f, float *est, float *H, float (*red)[MATCH_WAVES][9],
-                                            int parity, int *clamps, unsigned *nb_key, float4 *nb_val)
+                                            int parity, int *clamps, unsigned *nb_key, float4 *nb_val,
+                                            unsigned short *mlist)
 {
     const int tid = threadIdx.x;
     const float cs = sdm_cosf(est[2]);
@@ -321,28 +348,42 @@ __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, con
             }
         }
     }
+    // park the gathered log-odds of every miss in its slot, list the slot for its wave
+    const int lane = tid & 63;
+    unsigned short *wl = mlist + (tid >> 6) * (NP * 64);
+    int nmiss = 0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int slot = tid + j * MATCH_THREADS;
+        const unsigned long long bm = __ballot(miss[j]);
+        if (miss[j]) {
+            nb_val[slot] = make_float4(pf[j].l[0], pf[j].l[1], pf[j].l[2], pf[j].l[3]);
+            nb_key[slot] = key[j];
+            wl[nmiss + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] =
+                (unsigned short)slot;
+        }
+        nmiss += __popcll(bm);
+    }
+    // the wave's own LDS writes are seen by its later LDS reads (in-order per wave); keep the compiler
+    // from moving the reads above them
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int e = lane; e < nmiss; e += 64) {
+        const int slot = wl[e];
+        const float4 v = nb_val[slot];
+        nb_val[slot] = make_float4(cell_prob(v.x), cell_prob(v.y), cell_prob(v.z), cell_prob(v.w));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
         const int slot = tid + j * MATCH_THREADS;
         if (slot >= n) continue;
         if (pf[j].in) {
-            if (miss[j]) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) pf[j].l[q] = cell_prob(pf[j].l[q]);
-                nb_val[slot] = make_float4(pf[j].l[0], pf[j].l[1], pf[j].l[2], pf[j].l[3]);
-                nb_key[slot] = key[j];
-            } else {
-                const float4 v = nb_val[slot];
-                pf[j].l[0] = v.x; pf[j].l[1] = v.y; pf[j].l[2] = v.z; pf[j].l[3] = v.w;
-            }
+            const float4 v = nb_val[slot];
+            pf[j].l[0] = v.x; pf[j].l[1] = v.y; pf[j].l[2] = v.z; pf[j].l[3] = v.w;
         }
         point_accum<true>(pf[j], cs, sn, acc);
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) acc[k] = acc[k] + __shfl_xor(acc[k], off, 64);
-    }
+    wave_butterfly(acc);  // 64-lane xor butterfly, offsets 32..1
     const int wave = tid >> 6;
     if ((tid & 63) == 0) {
 #pragma unroll
@@ -393,6 +434,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     __shared__ float red[2][MATCH_WAVES][9];
     __shared__ unsigned nb_key[MATCH_REG_PTS * MATCH_THREADS];
     __shared__ float4 nb_val[MATCH_REG_PTS * MATCH_THREADS];
+    __shared__ unsigned short mlist[MATCH_REG_PTS * MATCH_THREADS];  // per wave: slots whose cell moved
     const int local = blockIdx.x;
     const int s = stream_begin + local;
     StreamState &st = state[s];
@@ -439,7 +481,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             for (int it = 0; it <= iters; ++it) {
                 if (in_regs)
                     gn_step_reg<MATCH_REG_PTS>(lc, g, preg, n, g.pts_scale, est, H, red, parity, &clamps, nb_key,
-                                               nb_val);
+                                               nb_val, mlist);
                 else
                     gn_step(lc, g, pts, n, g.pts_scale, est, H, red, parity, &clamps);
                 parity ^= 1;

@@ -10,6 +10,10 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   plain      WRONG RESULTS  hs_update_kernel marks with plain LDS stores instead of atomicMin
   noapply    WRONG RESULTS  hs_update_kernel skips the apply phase (no global loads / stores)
   hwexp      WRONG RESULTS  hs_match_kernel uses the hardware exp instead of (float)exp(double)
+  nowalk     WRONG RESULTS  hs_update_kernel clips every ray to the tile but skips the Bresenham walk
+  visits     same results   hs_update_kernel counts, per (tile, fan group) visit, the lanes with steps,
+                            the steps and the wave's longest walk into g_stamps[0..3]
+                            (hs_get_queue_stats out[4..7]; tools/diag_update.py prints them)
 """
 import os
 import shutil
@@ -27,6 +31,23 @@ PATCHES = {
                "{ *reinterpret_cast<volatile unsigned *>(p) = ev; }")],
     "noapply": [(K, "        if (pend_tl) {\n", "        if (pend_tl && false) {\n")],
     "hwexp": [(K, "    float odds = sdm_expf(l);", "    float odds = __expf(l);")],
+    "nowalk": [(K, "                if (scnt <= 0) continue;\n", "                continue;\n")],
+    "visits": [(K, "                if (scnt <= 0) continue;\n",
+                "                {\n"
+                "                    const unsigned long long am = __ballot(scnt > 0);\n"
+                "                    int mx = scnt, sm = scnt;\n"
+                "                    for (int off = 32; off >= 1; off >>= 1) {\n"
+                "                        mx = max(mx, __shfl_xor(mx, off, 64));\n"
+                "                        sm += __shfl_xor(sm, off, 64);\n"
+                "                    }\n"
+                "                    if (lane == 0) {\n"
+                "                        atomicAdd(&g_stamps[0], 1ull);\n"
+                "                        atomicAdd(&g_stamps[1], (unsigned long long)__popcll(am));\n"
+                "                        atomicAdd(&g_stamps[2], (unsigned long long)sm);\n"
+                "                        atomicAdd(&g_stamps[3], (unsigned long long)mx);\n"
+                "                    }\n"
+                "                }\n"
+                "                if (scnt <= 0) continue;\n")],
 }
 
 

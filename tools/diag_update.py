@@ -23,9 +23,7 @@ q = f.queue_stats(); kt = f.kernel_times()
 print("kernel ms:", kt)
 tot = q["cyc_setup"] + q["cyc_raster"] + q["cyc_apply"]
 blocks = B * (1 if os.environ.get("LVL_ONLY") else 3)
-print("per block: setup %.0f raster %.0f apply %.0f cycles; nonempty tiles/block %.1f" % (
-    q["cyc_setup"] / blocks, q["cyc_raster"] / blocks, q["cyc_apply"] / blocks, q["tiles"] / blocks))
-print("shares: setup %.3f raster %.3f apply %.3f" % (q["cyc_setup"] / tot, q["cyc_raster"] / tot, q["cyc_apply"] / tot))
-if os.environ.get("VISITS"):
-    print("group visits %d, active lanes/visit %.1f, steps/visit %.1f, max steps/visit %.1f, lane util %.3f" % (
-        q["items"], q["segments"] / q["items"], q["whole"] / q["items"], q["overflow"] / q["items"], q["whole"] / (64.0 * q["overflow"])))
+if os.environ.get("VISITS"):  # SLAM2D_LIB=.../libslam2d_visits.so (tools/build_diag.py visits)
+    v, a, st, mx = q["cyc_setup"], q["cyc_raster"], q["cyc_apply"], q["tiles"]
+    print("(tile, fan group) visits %d per scan %.1f; active lanes/visit %.1f, steps/visit %.1f, longest walk/visit "
+          "%.1f, walk lane utilisation %.3f" % (v, v / B, a / v, st / v, mx / v, st / (64.0 * mx)))

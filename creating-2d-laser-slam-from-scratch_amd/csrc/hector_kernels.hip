@@ -1474,8 +1474,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             if (__ballot(any) && lane == 0) s_any[buf] = 1u;
         }
         if (pend_tl) {
-            // apply the previous tile: log-odds of every marked cell, both planes written per marked
-            // cell (whole 16-B stores for fully marked quads); the updateIndex plane is never read --
+            // apply the previous tile: log-odds of every marked cell, both planes written (see below);
+            // the updateIndex plane is never read --
             // a cell's stored index always predates this scan's marks (currUpdateIndex += 3 per scan)
             int *tu = reinterpret_cast<int *>(pend_tl + TILE_CELLS);
 #pragma unroll
@@ -1490,19 +1490,20 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 int uv[4];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    nv[c] = apply_cell(lv[c], (mb >> (4 + c)) & 1u, (mb >> (8 + c)) & 1u, lf, lo);
+                    nv[c] = ((mb >> c) & 1u) ? apply_cell(lv[c], (mb >> (4 + c)) & 1u, (mb >> (8 + c)) & 1u, lf, lo)
+                                             : lv[c];
                     uv[c] = ((mb >> (8 + c)) & 1u) ? mark_occ : mark_free;
                 }
+                // log-odds: the whole quad was loaded, so it is stored whole (one instruction; unmarked
+                // cells rewrite their own value); updateIndex: whole when every cell is marked, else
+                // per marked cell (its unmarked cells were never read)
+                *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);
                 if ((mb & 15u) == 15u) {
-                    *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);
                     *reinterpret_cast<int4 *>(&tu[o]) = make_int4(uv[0], uv[1], uv[2], uv[3]);
                 } else {
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        if ((mb >> c) & 1u) {
-                            pend_tl[o + c] = nv[c];
-                            tu[o + c] = uv[c];
-                        }
+                        if ((mb >> c) & 1u) tu[o + c] = uv[c];
                 }
                 touched += __popc(mb & 15u);
             }

@@ -38,6 +38,15 @@ __device__ __forceinline__ unsigned gm_udiv(unsigned n, unsigned d)
     return q;
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations but not for its global
+// stores (__syncthreads' release fence drains vmcnt, which parked every wave on the previous tile's
+// 8 KB of count stores at each tile: 72 % of wave cycles waiting, r02o PMC).  The stores go to the
+// particle's own map, which no wave of this kernel reads.
+__device__ __forceinline__ void gm_lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 constexpr int GM_STRIDE = 68;                          // LDS words per tile row (16-B rows)
 constexpr int GM_LDS_WORDS = GM_TILE_H * GM_STRIDE;    // one LDS tile array
 
@@ -211,6 +220,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
     float2 *hitxy = reinterpret_cast<float2 *>(rays + ((n + 3) & ~3));   // (float)hit point
     int4 *gbox = reinterpret_cast<int4 *>(hitxy + ((n + 1) & ~1));      // per 64-beam fan group
     __shared__ int s_box[4];
+    __shared__ int s_anyf[2];   // per tile parity: "some lane marked a cell"
 
     const int part = blockIdx.x / count;
     const int local = blockIdx.x - part * count;
@@ -273,7 +283,8 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
 
     long long nfree = 0;
     const int ntx = tx1 - tx0 + 1, ntiles = (tx1 >= tx0) ? ntx * (ty1 - ty0 + 1) : 0;
-    for (int t = part; t < ntiles; t += parts) {
+    int it = 0;
+    for (int t = part; t < ntiles; t += parts, ++it) {
         const int tx = tx0 + t % ntx, ty = ty0 + t / ntx;
         const int X0 = tx * GM_TILE, Y0 = ty * GM_TILE_H;
         const int X1 = min(X0 + GM_TILE, g.sx), Y1 = min(Y0 + GM_TILE_H, g.sy);
@@ -281,7 +292,9 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
             reinterpret_cast<uint4 *>(cnt)[k] = make_uint4(0u, 0u, 0u, 0u);
             reinterpret_cast<uint4 *>(first_hit)[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
         }
-        __syncthreads();
+        // the flag of this parity was last read two tiles ago, with barriers in between
+        if (tid == 0) s_anyf[it & 1] = 0;
+        gm_lds_barrier();
         for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
             const int4 gb = gbox[b0 >> 6];
             const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
@@ -334,8 +347,10 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
             }
             if (i < steps) atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);
         }
+        if (__ballot(any_tile_marks) && (tid & 63) == 0) reinterpret_cast<volatile int *>(s_anyf)[it & 1] = 1;
+        gm_lds_barrier();
         // tiles without any mark are not written: their stale stamp makes them read as fresh
-        if (!__syncthreads_or(any_tile_marks)) continue;
+        if (!reinterpret_cast<volatile int *>(s_anyf)[it & 1]) continue;
         any_tile_marks = false;
         unsigned *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
         // acc: the first hitting beam of a cell sums every hit of that cell in beam order (:236-240)
@@ -355,13 +370,15 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
             float ax = 0.0f, ay = 0.0f;
             ax += hitxy[b].x;
             ay += hitxy[b].y;
-            if ((cnt[c] >> 16) > 1) {
-                for (int b2 = b + 1; b2 < n; ++b2)
-                    if (rays[b2] == r) {
-                        ax += hitxy[b2].x;
-                        ay += hitxy[b2].y;
-                    }
-            }
+            // the other hits of the cell, in beam order; the raster counted them (n = cnt >> 16), so the
+            // scan stops at the last one -- they are nearly always the next beams (a long serial scan
+            // of every later beam per multiply-hit cell was most of this kernel's time)
+            for (int need = (int)(cnt[c] >> 16) - 1, b2 = b + 1; need > 0 && b2 < n; ++b2)
+                if (rays[b2] == r) {
+                    ax += hitxy[b2].x;
+                    ay += hitxy[b2].y;
+                    --need;
+                }
             GmHitCell hc;
             hc.cell = y1 * g.sx + x1;
             hc.ax = ax;
@@ -375,7 +392,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
                 *reinterpret_cast<const uint4 *>(&cnt[row * GM_STRIDE + c4]);
         }
         if (tid == 0) pstamp[ty * g.tiles_x + tx] = cur_step;
-        __syncthreads();
+        gm_lds_barrier();  // the tile's LDS counts are read before the next tile clears them
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) nfree += __shfl_xor(nfree, off, 64);

@@ -10,6 +10,8 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   plain      WRONG RESULTS  hs_update_kernel marks with plain LDS stores instead of atomicMin
   noapply    WRONG RESULTS  hs_update_kernel skips the apply phase (no global loads / stores)
   hwexp      WRONG RESULTS  hs_match_kernel uses the hardware exp instead of (float)exp(double)
+  gmplain    WRONG RESULTS  gm_compute_kernel walks with plain LDS stores instead of atomicAdd
+  gmnowalk   WRONG RESULTS  gm_compute_kernel clips every line to the tile but skips the walk
   nowalk     WRONG RESULTS  hs_update_kernel clips every ray to the tile but skips the Bresenham walk
   visits     same results   hs_update_kernel counts, per (tile, fan group) visit, the lanes with steps,
                             the steps and the wave's longest walk into g_stamps[0..3]
@@ -31,6 +33,12 @@ PATCHES = {
                "{ *reinterpret_cast<volatile unsigned *>(p) = ev; }")],
     "noapply": [(K, "        if (pend_tl) {\n", "        if (pend_tl && false) {\n")],
     "hwexp": [(K, "    float odds = sdm_expf(l);", "    float odds = __expf(l);")],
+    "gmplain": [("gmapping_kernels.hip", "            for (; i + 1 < steps; i += 2) {\n                atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);",
+                 "            for (; i + 1 < steps; i += 2) {\n                *reinterpret_cast<volatile unsigned *>(pc) = 1u;"),
+                ("gmapping_kernels.hip", "                pc += dab + (m & dbb);\n                atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);",
+                 "                pc += dab + (m & dbb);\n                *reinterpret_cast<volatile unsigned *>(pc) = 1u;")],
+    "gmnowalk": [("gmapping_kernels.hip", "            int i = 0;\n            for (; i + 1 < steps; i += 2) {",
+                  "            int i = steps;\n            for (; i + 1 < steps; i += 2) {")],
     "nowalk": [(K, "                if (scnt <= 0) continue;\n", "                continue;\n")],
     "visits": [(K, "                if (scnt <= 0) continue;\n",
                 "                {\n"

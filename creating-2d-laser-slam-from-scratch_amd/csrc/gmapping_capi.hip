@@ -37,9 +37,13 @@ int gfail(int code, const char *what, hipError_t e = hipSuccess)
 
 struct gm_ctx {
     int P = 0, max_beams = 0, n_beams = 0;
-    int parts = 8;  // gm_compute_kernel workgroups per particle (SLAM2D_GM_PARTS; 2: 670k, 4: 716k, 8: 757k, 16: 747k particle-scans/s)
+    // gm_compute_kernel workgroups per particle (SLAM2D_GM_PARTS): r02 sweep, 1024 particles:
+    // 3: 1.24 M, 4: 1.25 M, 5: 1.25 M, 6: 1.25 M, 8: 1.23 M, 12: 1.14 M, 16: 1.11 M particle-scans/s
+    int parts = 5;
     GmGeom geom{};
     unsigned *d_maps = nullptr;   // packed counts, tiled
+    unsigned *d_rays = nullptr;   // per particle, per beam: packed end cell (gm_score_kernel -> gm_compute_kernel)
+    float2 *d_hitxy = nullptr;    // per particle, per beam: (float) hit point
     int *d_stamps = nullptr;      // per particle, per tile
     GmHitCell *d_hits = nullptr;  // per particle, max_beams entries
     GmState *d_state = nullptr;
@@ -57,8 +61,7 @@ struct gm_ctx {
 namespace {
 size_t gm_shmem(int n)
 {
-    return sizeof(unsigned) * (2 * (size_t)GM_LDS_WORDS + (size_t)((n + 3) & ~3)) + sizeof(float2) * (size_t)((n + 1) & ~1) +
-           sizeof(int4) * (size_t)((n + 63) / 64);
+    return sizeof(unsigned) * (2 * (size_t)GM_LDS_WORDS + (size_t)((n + 3) & ~3)) + sizeof(int4) * (size_t)((n + 63) / 64);
 }
 
 int reset_state(gm_ctx *c)
@@ -89,11 +92,10 @@ int launch(gm_ctx *c, int begin, int count, const double *d_poses, const float *
         GCHK(hipEventRecord(ev.first, s));
     }
     hipLaunchKernelGGL(gm_score_kernel, dim3(count), dim3(GM_THREADS), 0, s, c->geom, d_poses, d_ranges, n, c->d_cos,
-                       c->d_sin, c->d_maps, c->d_stamps, c->d_state, d_scores, begin);
+                       c->d_sin, c->d_maps, c->d_stamps, c->d_state, d_scores, begin, c->d_rays, c->d_hitxy);
     GCHK(hipGetLastError());
     hipLaunchKernelGGL(gm_compute_kernel, dim3(count * c->parts), dim3(GM_THREADS), gm_shmem(n), s, c->geom, d_poses,
-                       d_ranges, n, c->d_cos, c->d_sin, c->d_maps, c->d_stamps, c->d_hits, c->d_state, begin, count,
-                       c->parts);
+                       n, c->d_rays, c->d_hitxy, c->d_maps, c->d_stamps, c->d_hits, c->d_state, begin, count, c->parts);
     GCHK(hipGetLastError());
     if (c->timing) {
         GCHK(hipEventRecord(ev.second, s));
@@ -149,6 +151,8 @@ int gm_create(gm_ctx **out, int num_particles, int max_beams, double xmin, doubl
     }
     if ((e = hipMalloc(&c->d_maps, sizeof(unsigned) * g.particle_words * (size_t)c->P)) != hipSuccess ||
         (e = hipMalloc(&c->d_stamps, sizeof(int) * (size_t)g.ntiles * c->P)) != hipSuccess ||
+        (e = hipMalloc(&c->d_rays, sizeof(unsigned) * (size_t)max_beams * c->P)) != hipSuccess ||
+        (e = hipMalloc(&c->d_hitxy, sizeof(float2) * (size_t)max_beams * c->P)) != hipSuccess ||
         (e = hipMalloc(&c->d_hits, sizeof(GmHitCell) * (size_t)max_beams * c->P)) != hipSuccess ||
         (e = hipMalloc(&c->d_state, sizeof(GmState) * c->P)) != hipSuccess ||
         (e = hipMalloc(&c->d_cos, sizeof(double) * max_beams)) != hipSuccess ||
@@ -173,6 +177,8 @@ int gm_destroy(gm_ctx *c)
     if (!c) return GM_OK;
     if (c->stream) hipStreamSynchronize(c->stream);
     hipFree(c->d_maps);
+    hipFree(c->d_rays);
+    hipFree(c->d_hitxy);
     hipFree(c->d_stamps);
     hipFree(c->d_hits);
     hipFree(c->d_state);

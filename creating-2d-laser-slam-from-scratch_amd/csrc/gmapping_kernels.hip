@@ -147,11 +147,14 @@ __device__ __forceinline__ GmBeam gm_beam(const GmGeom &g, double px, double py,
 // Particle weight (build-defined, the reference has no particles): hit beams of this scan whose
 // end cell is occupied (n/visits > occ_thresh, map.h:27 + gmapping.cc:150) in the particle's
 // previous map.  Runs before gm_compute_kernel overwrites that map; opens the particle's new step.
+// It also leaves the particle's rays for gm_compute_kernel: the packed end cell relative to p0 (or
+// GM_RAY_INVALID) and the (float) hit point of every beam, so the compute workgroups of the particle
+// neither redo the double-precision end points nor keep the hit points in LDS.
 __global__ void __launch_bounds__(GM_THREADS)
 gm_score_kernel(GmGeom g, const double *__restrict__ poses, const float *__restrict__ ranges, int n,
                 const double *__restrict__ a_cos, const double *__restrict__ a_sin, const unsigned *__restrict__ maps,
                 const int *__restrict__ stamps, GmState *__restrict__ state, int *__restrict__ scores_out,
-                int particle_begin)
+                int particle_begin, unsigned *__restrict__ rays_out, float2 *__restrict__ hitxy_out)
 {
     __shared__ int s_red[GM_THREADS / 64][2];
     const int p = particle_begin + blockIdx.x;
@@ -163,9 +166,18 @@ gm_score_kernel(GmGeom g, const double *__restrict__ poses, const float *__restr
     const int ptx0 = st.tx0, pty0 = st.ty0, ptx1 = st.tx1, pty1 = st.ty1;  // previous map's box
     const double px = poses[4 * blockIdx.x], py = poses[4 * blockIdx.x + 1];
     const double ct = poses[4 * blockIdx.x + 2], sn = poses[4 * blockIdx.x + 3];
+    int x0, y0;
+    gm_world2map(g, px, py, x0, y0);  // p0 = world2map(lp) (:176-179)
+    unsigned *prays = rays_out + (size_t)p * g.max_beams;
+    float2 *phxy = hitxy_out + (size_t)p * g.max_beams;
     int score = 0, hits = 0;
     for (int b = tid; b < n; b += GM_THREADS) {
         const GmBeam e = gm_beam(g, px, py, ct, sn, ranges[b], a_cos[b], a_sin[b]);
+        unsigned r = GM_RAY_INVALID;
+        // lines longer than 16383 cells are not representable (max_range / delta < 16384)
+        if (e.valid && abs(e.x1 - x0) < GM_REL && abs(e.y1 - y0) < GM_REL) r = gm_pack(e.x1 - x0, e.y1 - y0, e.hit);
+        prays[b] = r;
+        phxy[b] = make_float2((float)e.wx, (float)e.wy);
         if (!e.valid || !e.hit) continue;
         hits += 1;
         const int x1 = e.x1, y1 = e.y1;
@@ -208,17 +220,16 @@ gm_score_kernel(GmGeom g, const double *__restrict__ poses, const float *__restr
 // Grid: parts x count workgroups (part-major); part q draws tiles q, q + parts, ... of the particle's
 // tile box.  Runs after gm_score_kernel of the same step.
 __global__ void __launch_bounds__(GM_THREADS)
-gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__restrict__ ranges, int n,
-                  const double *__restrict__ a_cos, const double *__restrict__ a_sin, unsigned *__restrict__ maps,
-                  int *__restrict__ stamps, GmHitCell *__restrict__ hit_cells, GmState *__restrict__ state,
-                  int particle_begin, int count, int parts)
+gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsigned *__restrict__ rays_in,
+                  const float2 *__restrict__ hitxy, unsigned *__restrict__ maps, int *__restrict__ stamps,
+                  GmHitCell *__restrict__ hit_cells, GmState *__restrict__ state, int particle_begin, int count,
+                  int parts)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned smem[];
     unsigned *cnt = smem;                              // n << 16 | visits per cell of the tile
     unsigned *first_hit = smem + GM_LDS_WORDS;         // lowest hitting beam per cell
     unsigned *rays = smem + 2 * GM_LDS_WORDS;          // packed end cells
-    float2 *hitxy = reinterpret_cast<float2 *>(rays + ((n + 3) & ~3));   // (float)hit point
-    int4 *gbox = reinterpret_cast<int4 *>(hitxy + ((n + 1) & ~1));      // per 64-beam fan group
+    int4 *gbox = reinterpret_cast<int4 *>(rays + ((n + 3) & ~3));        // per 64-beam fan group
     __shared__ int s_box[4];
     __shared__ int s_anyf[2];   // per tile parity: "some lane marked a cell"
 
@@ -232,29 +243,26 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
     GmState &st = state[p];
     const int cur_step = st.step;
     const double px = poses[4 * local], py = poses[4 * local + 1];
-    const double ct = poses[4 * local + 2], sn = poses[4 * local + 3];
     int x0, y0;
     gm_world2map(g, px, py, x0, y0);  // p0 = world2map(lp) (:176-179)
+    const unsigned *prays = rays_in + (size_t)p * g.max_beams;
+    const float2 *phxy = hitxy + (size_t)p * g.max_beams;  // (float) hit points, read by the hit pass only
 
     if (tid == 0) {
         s_box[0] = g.sx; s_box[1] = g.sy; s_box[2] = -1; s_box[3] = -1;
     }
     __syncthreads();
-    // ---- rays (:185-214)
+    // ---- rays (:185-214), computed by gm_score_kernel
     int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
     for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
         const int b = b0 + (tid & 63);
         unsigned r = GM_RAY_INVALID;
         int gx0 = x0, gy0 = y0, gx1 = x0, gy1 = y0;
         if (b < n) {
-            const GmBeam e = gm_beam(g, px, py, ct, sn, ranges[b], a_cos[b], a_sin[b]);
-            if (e.valid) {
-                hitxy[b] = make_float2((float)e.wx, (float)e.wy);
-                // lines longer than 16383 cells are not representable (max_range / delta < 16384)
-                if (abs(e.x1 - x0) < GM_REL && abs(e.y1 - y0) < GM_REL) {
-                    r = gm_pack(e.x1 - x0, e.y1 - y0, e.hit);
-                    gx0 = min(gx0, e.x1); gy0 = min(gy0, e.y1); gx1 = max(gx1, e.x1); gy1 = max(gy1, e.y1);
-                }
+            r = prays[b];
+            if (r != GM_RAY_INVALID) {
+                const int x1 = x0 + (int)(r & 0xFFFFu) - GM_REL, y1 = y0 + (int)((r >> 16) & 0x7FFFu) - GM_REL;
+                gx0 = min(gx0, x1); gy0 = min(gy0, y1); gx1 = max(gx1, x1); gy1 = max(gy1, y1);
             }
             rays[b] = r;
         }
@@ -368,15 +376,17 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, const float *__res
             const int c = (y1 - Y0) * GM_STRIDE + (x1 - X0);
             if (first_hit[c] != (unsigned)b) continue;
             float ax = 0.0f, ay = 0.0f;
-            ax += hitxy[b].x;
-            ay += hitxy[b].y;
+            const float2 h0 = phxy[b];
+            ax += h0.x;
+            ay += h0.y;
             // the other hits of the cell, in beam order; the raster counted them (n = cnt >> 16), so the
             // scan stops at the last one -- they are nearly always the next beams (a long serial scan
             // of every later beam per multiply-hit cell was most of this kernel's time)
             for (int need = (int)(cnt[c] >> 16) - 1, b2 = b + 1; need > 0 && b2 < n; ++b2)
                 if (rays[b2] == r) {
-                    ax += hitxy[b2].x;
-                    ay += hitxy[b2].y;
+                    const float2 h2 = phxy[b2];
+                    ax += h2.x;
+                    ay += h2.y;
                     --need;
                 }
             GmHitCell hc;

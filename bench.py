@@ -253,7 +253,7 @@ def run_gmapping(args, world, rank, dev):
     import torch.distributed as dist
 
     from slam2d import synth
-    from slam2d.gmapping import GMappingFleet, normalize_weights
+    from slam2d.gmapping import GMappingFleet, RcclComm, normalize_weights
 
     P_total = args.particles
     P = P_total // world + (1 if rank < P_total % world else 0)
@@ -271,9 +271,22 @@ def run_gmapping(args, world, rank, dev):
     fleet.set_beams(ang)
     hs = torch.cuda.current_stream(dev).cuda_stream
     nb = ranges.shape[1]
+    c_weights = args.weights == "capi"
+    comm = None
+    if c_weights and world > 1:
+        def bcast(buf):  # the RCCL unique id from rank 0, over the job's process group
+            t = torch.from_numpy(buf).to(dev)
+            dist.broadcast(t, 0)
+            return t.cpu().numpy()
+        comm = RcclComm(world, rank, bcast)
+    d_w = torch.zeros(P, dtype=torch.float64, device=dev)
+    d_sums = torch.zeros(2, dtype=torch.float64, device=dev)
 
     def step(t):
         fleet.compute_device(d_poses[t].data_ptr(), d_ranges[t].data_ptr(), nb, d_scores.data_ptr(), hip_stream=hs)
+        if c_weights:  # gm_normalize_weights_device: ONE RCCL all-reduce of 2 doubles inside the C-ABI
+            fleet.normalize_weights_device(comm, d_scores.data_ptr(), P, d_w.data_ptr(), d_sums.data_ptr(), hip_stream=hs)
+            return d_w, None
         return normalize_weights(d_scores)
 
     for t in range(W):
@@ -289,6 +302,9 @@ def run_gmapping(args, world, rank, dev):
     for t in range(W, T):
         _, neff = step(t)
     torch.cuda.synchronize()
+    if neff is None:
+        sums = d_sums.cpu().numpy()
+        neff = float(sums[0] * sums[0] / sums[1])
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -315,6 +331,8 @@ def run_gmapping(args, world, rank, dev):
                "vs_baseline": None, "dtype": "int32+f64", "data": "synthetic",
                "config": {"workload": f"make_gmapping_map ComputeMap, 1600x1600 @0.05 m fresh map per scan, "
                                       f"{P_total} particles x 1081 beams, weights all-reduced every step",
+                          "weights": ("gm_normalize_weights_device (C-ABI, RCCL all-reduce)" if c_weights
+                                      else "torch.distributed all_reduce"),
                           "config": "gmapping", "particles": P_total, "particles_per_gpu": P,
                           "parallelism": f"particles sharded x{world}"},
                "roofline": roof, "cpu_baseline": cpu, "neff": neff}
@@ -577,6 +595,9 @@ def main():
     ap.add_argument("--pairs", type=int, default=2048, help="plicp: scan pairs per GPU per step")
     ap.add_argument("--matches", type=int, default=0, help="karto: MatchScan calls per GPU per step (0 = default)")
     ap.add_argument("--particles", type=int, default=1024, help="gmapping: particles of the whole job")
+    ap.add_argument("--weights", choices=["capi", "torch"], default="capi",
+                    help="gmapping: particle-weight exchange through gm_normalize_weights_device (RCCL inside the "
+                         "C-ABI) or the Python torch.distributed path")
     ap.add_argument("--karto-shard", action="store_true",
                     help="karto: split every match's coarse window over the GPUs (one RCCL all-reduce per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -2,6 +2,7 @@
 // GMapping particle-map path.  Every compute step is gm_compute_kernel (gmapping_kernels.hip);
 // without a usable HIP device gm_create fails with GM_ENODEV.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <math.h>
 #include <stdlib.h>
@@ -246,6 +247,30 @@ int gm_compute_maps_device(gm_ctx *c, int begin, int count, const double *d_pose
     if (n < 0 || n > c->n_beams) return gfail(GM_EINVAL, "n exceeds the beam cache (gm_set_beams)");
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
     return launch(c, begin, count, d_poses, d_ranges, n, d_scores_out, s);
+}
+
+int gm_normalize_weights_device(gm_ctx *c, void *nccl_comm, const int32_t *d_scores, int count, double *d_weights_out,
+                                double *d_sums_out, void *hip_stream)
+{
+    if (!c || !d_sums_out || (count > 0 && !d_scores)) return gfail(GM_EINVAL, "NULL argument");
+    if (count < 0) return gfail(GM_EINVAL, "count < 0");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipLaunchKernelGGL(gm_weight_sums_kernel, dim3(1), dim3(GM_THREADS), 0, s, d_scores, count, d_sums_out);
+    GCHK(hipGetLastError());
+    if (nccl_comm) {
+        // the one exchange of the sharded particle set: 2 doubles, summed over the ranks (RCCL over xGMI)
+        const ncclResult_t r = ncclAllReduce(d_sums_out, d_sums_out, 2, ncclDouble, ncclSum, (ncclComm_t)nccl_comm, s);
+        if (r != ncclSuccess) {
+            gm_err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+            return GM_EHIP;
+        }
+    }
+    if (d_weights_out && count > 0) {
+        hipLaunchKernelGGL(gm_weights_kernel, dim3((count + 255) / 256), dim3(256), 0, s, d_scores, count, d_sums_out,
+                           d_weights_out);
+        GCHK(hipGetLastError());
+    }
+    return GM_OK;
 }
 
 int gm_get_particle_map(gm_ctx *c, int p, int32_t *n_out, int32_t *visits_out, float *acc_out)

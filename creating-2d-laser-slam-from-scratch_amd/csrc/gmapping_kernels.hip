@@ -409,6 +409,48 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
     if ((tid & 63) == 0 && nfree) atomicAdd(reinterpret_cast<unsigned long long *>(&st.free_updates), (unsigned long long)nfree);
 }
 
+// Particle weights, local half of the exchange: sums[0] = Σ (score + 1), sums[1] = Σ (score + 1)^2 over
+// this rank's particles, as doubles.  Every term is an integer below 2^53, so the sums are exact and
+// independent of the summation order (and of how the particles are sharded over ranks).
+__global__ void __launch_bounds__(GM_THREADS) gm_weight_sums_kernel(const int *__restrict__ scores, int count,
+                                                                    double *__restrict__ sums)
+{
+    __shared__ double s_red[GM_THREADS / 64][2];
+    double a = 0.0, q = 0.0;
+    for (int i = threadIdx.x; i < count; i += GM_THREADS) {
+        const double v = (double)scores[i] + 1.0;
+        a += v;
+        q += v * v;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        a += __shfl_xor(a, off, 64);
+        q += __shfl_xor(q, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_red[threadIdx.x >> 6][0] = a;
+        s_red[threadIdx.x >> 6][1] = q;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double ta = 0.0, tq = 0.0;
+        for (int w = 0; w < GM_THREADS / 64; ++w) {
+            ta += s_red[w][0];
+            tq += s_red[w][1];
+        }
+        sums[0] = ta;
+        sums[1] = tq;
+    }
+}
+
+// w_p = (score_p + 1) / Σ_all (score + 1), from the all-reduced sums
+__global__ void gm_weights_kernel(const int *__restrict__ scores, int count, const double *__restrict__ sums,
+                                  double *__restrict__ w)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) w[i] = ((double)scores[i] + 1.0) / sums[0];
+}
+
 // GMapping::PublishMap conversion (gmapping.cc:141-159): -1 unvisited, 100 if n/visits > thresh, 0
 __global__ void gm_publish_kernel(const unsigned *__restrict__ pm, const int *__restrict__ pstamp, GmGeom g, int step,
                                   int8_t *__restrict__ out)

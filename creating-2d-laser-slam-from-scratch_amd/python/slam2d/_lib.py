@@ -84,6 +84,7 @@ def _declare(L):
     L.gm_get_scores.argtypes = [_p, _p, _p, _p]
     L.gm_set_timing.argtypes = [_p, _i]
     L.gm_get_kernel_times.argtypes = [_p, _p, _p, _i]
+    L.gm_normalize_weights_device.argtypes = [_p, _p, _p, _i, _p, _p, _p]
 
 
 def lib() -> C.CDLL:

@@ -92,6 +92,16 @@ class GMappingFleet:
                                                      int(n), C.c_void_p(d_scores or None),
                                                      C.c_void_p(hip_stream or None)), "gm_compute_maps_device")
 
+    def normalize_weights_device(self, comm, d_scores: int, count: int, d_weights: int, d_sums: int,
+                                 hip_stream: int = 0):
+        """gm_normalize_weights_device: [Σ(s+1), Σ(s+1)^2] of this rank's scores all-reduced with RCCL on
+        `comm` (an RcclComm or None for a single rank), weights (double[count]) and sums (double[2])."""
+        _check(self.L, self.L.gm_normalize_weights_device(self.h, C.c_void_p(comm.handle if comm else None),
+                                                          C.c_void_p(d_scores), int(count),
+                                                          C.c_void_p(d_weights or None), C.c_void_p(d_sums),
+                                                          C.c_void_p(hip_stream or None)),
+               "gm_normalize_weights_device")
+
     def particle_map(self, p: int):
         sx, sy = self.size
         n = np.empty(sx * sy, np.int32)
@@ -142,3 +152,40 @@ def normalize_weights(scores, group=None):
     w = s / total
     neff = (total * total) / sq
     return w, float(neff)
+
+
+class _UniqueId(C.Structure):
+    _fields_ = [("internal", C.c_char * 128)]   # ncclUniqueId (rccl.h: NCCL_UNIQUE_ID_BYTES)
+
+
+class RcclComm:
+    """An RCCL communicator over the ranks of the job, made the way a C++ host would make one
+    (ncclGetUniqueId on rank 0, ncclCommInitRank everywhere); the unique id travels over `bcast`
+    (a callable broadcasting a uint8 numpy array from rank 0, e.g. over torch.distributed).  Its
+    handle is what gm_normalize_weights_device takes as `nccl_comm`."""
+
+    def __init__(self, world: int, rank: int, bcast=None):
+        self._R = C.CDLL("librccl.so.1")
+        self._R.ncclGetUniqueId.argtypes = [C.POINTER(_UniqueId)]
+        self._R.ncclCommInitRank.argtypes = [C.POINTER(C.c_void_p), C.c_int, _UniqueId, C.c_int]
+        self._R.ncclCommDestroy.argtypes = [C.c_void_p]
+        self._R.ncclGetErrorString.restype = C.c_char_p
+        uid = _UniqueId()
+        if rank == 0:
+            self._ok(self._R.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
+        if world > 1:
+            buf = np.frombuffer(bytes(uid.internal), np.uint8).copy() if rank == 0 else np.zeros(128, np.uint8)
+            buf = bcast(buf)
+            C.memmove(C.addressof(uid), buf.tobytes(), 128)
+        h = C.c_void_p()
+        self._ok(self._R.ncclCommInitRank(C.byref(h), int(world), uid, int(rank)), "ncclCommInitRank")
+        self.handle = h.value
+
+    def _ok(self, rc, what):
+        if rc != 0:
+            raise Slam2dError(f"{what} failed: {self._R.ncclGetErrorString(rc).decode()}")
+
+    def close(self):
+        if self.handle:
+            self._R.ncclCommDestroy(C.c_void_p(self.handle))
+            self.handle = None

@@ -10,7 +10,8 @@
  *
  * The build evaluates the scan for P candidate poses ("particles"; the reference uses the laser
  * frame itself, lp = (0,0,0), gmapping.cc:176).  Particles shard across GPUs (one context per
- * rank holding its particles); per-particle scores are reduced across ranks by the caller (RCCL).
+ * rank holding its particles); gm_normalize_weights_device performs the one RCCL all-reduce of the
+ * particle weights on a communicator the host passes in.
  *
  * Conventions as in hector.h: plain C types, int status (GM_OK / negative), gm_last_error().
  * Poses are double[4] per particle: x, y, cos(theta), sin(theta) (the caller evaluates the trig,
@@ -59,6 +60,17 @@ int gm_compute_maps(gm_ctx *ctx, const double *poses, const float *ranges, int n
  * d_ranges float[n], d_scores_out int32[count] or NULL; stream-ordered on hip_stream (NULL = own). */
 int gm_compute_maps_device(gm_ctx *ctx, int particle_begin, int count, const double *d_poses, const float *d_ranges,
                            int n, int32_t *d_scores_out, void *hip_stream);
+
+/* The particle-weight exchange of a particle set sharded over ranks (north_star "RCCL
+ * allreduce of particle weights"): from this rank's integer scores d_scores int32[count] (the
+ * gm_compute_maps_device output) form [Σ(score+1), Σ(score+1)^2] in double on the device, all-reduce
+ * them (sum) over the ranks of nccl_comm (an ncclComm_t as void*, RCCL; NULL = single rank, no
+ * exchange) on hip_stream, and write the normalised weights of this rank's particles
+ * w_p = (score_p + 1) / Σ_all (score + 1) to d_weights_out (double[count], may be NULL).  d_sums_out
+ * (device double[2]) receives the reduced sums; the effective sample size is sums[0]^2 / sums[1].
+ * All terms are integers below 2^53, so the result does not depend on the sharding. */
+int gm_normalize_weights_device(gm_ctx *ctx, void *nccl_comm, const int32_t *d_scores, int count,
+                                double *d_weights_out, double *d_sums_out, void *hip_stream);
 
 /* Dense row-major read-out of one particle's map (index y * size_x + x): n (hits), visits, acc
  * (2 floats per cell).  Any pointer may be NULL.  Synchronises. */

@@ -164,3 +164,34 @@ def test_device_entry_and_scores_buffer(gpu):
         s, _, _ = fleet.scores()
         np.testing.assert_array_equal(d_scores.cpu().numpy(), s)
         _check_maps(fleet, _oracle_maps(poses4, ranges, ang), P)
+
+
+@pytest.mark.parametrize("use_comm", [True, False])
+def test_normalize_weights_rccl_world1(gpu, use_comm):
+    """gm_normalize_weights_device: the C-ABI form of the particle-weight exchange, with a real RCCL
+    communicator made as a C++ host would (ncclGetUniqueId + ncclCommInitRank, world size 1 on the one
+    GPU of the box) or none.  Sums are exact integers in double, weights equal the Python
+    normalize_weights (torch) bit for bit; the world-2 exchange itself is covered with gloo
+    (tests/test_host_cpu.py)."""
+    import torch
+
+    from slam2d.gmapping import RcclComm, normalize_weights
+
+    P = 1000
+    fleet = GMappingFleet(4)
+    scores = torch.from_numpy(np.random.default_rng(3).integers(0, 900, P).astype(np.int32)).cuda()
+    w = torch.full((P,), -1.0, dtype=torch.float64, device="cuda")
+    sums = torch.zeros(2, dtype=torch.float64, device="cuda")
+    comm = RcclComm(1, 0) if use_comm else None
+    try:
+        fleet.normalize_weights_device(comm, scores.data_ptr(), P, w.data_ptr(), sums.data_ptr(),
+                                       hip_stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        if comm:
+            comm.close()
+    s = scores.cpu().numpy().astype(np.float64) + 1.0
+    assert sums.cpu().tolist() == [s.sum(), (s * s).sum()]
+    wt, neff = normalize_weights(scores)
+    np.testing.assert_array_equal(w.cpu().numpy(), wt.cpu().numpy())
+    assert neff == pytest.approx(s.sum() ** 2 / (s * s).sum(), rel=1e-15)

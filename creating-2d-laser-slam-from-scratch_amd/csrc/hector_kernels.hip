@@ -294,15 +294,19 @@ constexpr unsigned NB_NONE = 0xFFFFFFFFu;
 // point's cache slot and appends the slot to its wave's list; the wave then converts the listed slots
 // 64 at a time (4 exp + 4 divisions each) -- with per-slot branches the whole wave would pay the
 // conversion of slot j whenever ANY of its 64 lanes missed there, i.e. on nearly every step.
+// The step's uniform tail -- H / b from the wave sums, the 3x3 solve, the clamp, the new estimate and
+// the sin / cos (in double) of its angle for the next step -- runs on ONE wave of the workgroup (wave
+// blockIdx.x % 4, so the four SIMDs share the duty across workgroups) and is broadcast through LDS
+// (s_pose[parity]: est[3], cos, sin, H[9], clamp flag); the other waves would only repeat it.
+constexpr int POSE_WORDS = 16;
+
 template <int NP>
 __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
-                                            int n, float f, float *est, float *H, float (*red)[MATCH_WAVES][9],
-                                            int parity, int *clamps, unsigned *nb_key, float4 *nb_val,
-                                            unsigned short *mlist)
+                                            int n, float f, float *est, float &cs, float &sn, float *H,
+                                            float (*red)[MATCH_WAVES][9], int parity, unsigned *nb_key,
+                                            float4 *nb_val, unsigned short *mlist, float (*s_pose)[POSE_WORDS])
 {
     const int tid = threadIdx.x;
-    const float cs = sdm_cosf(est[2]);
-    const float sn = sdm_sinf(est[2]);
     float acc[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
@@ -390,31 +394,53 @@ __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, con
         for (int k = 0; k < 9; ++k) red[parity][wave][k] = acc[k];
     }
     __syncthreads();
-    float s[9];
+    float *sp = s_pose[parity];
+    if (wave == (int)(blockIdx.x & (MATCH_WAVES - 1))) {
+        float s[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        float a0 = red[parity][0][k] + red[parity][2][k];
-        float a1 = red[parity][1][k] + red[parity][3][k];
-        s[k] = a0 + a1;
-    }
-    float b[3] = {s[0], s[1], s[2]};
-    H[0] = s[3]; H[4] = s[4]; H[8] = s[5];
-    H[1] = s[6]; H[2] = s[7]; H[5] = s[8];
-    H[3] = H[1]; H[6] = H[2]; H[7] = H[5];
-    if ((H[0] != 0.0f) && (H[4] != 0.0f)) {
-        float d[3];
-        solve3(H, b, d);
-        if (d[2] > 0.2f) {
-            d[2] = 0.2f;
-            (*clamps)++;
-        } else if (d[2] < -0.2f) {
-            d[2] = -0.2f;
-            (*clamps)++;
+        for (int k = 0; k < 9; ++k) {
+            float a0 = red[parity][0][k] + red[parity][2][k];
+            float a1 = red[parity][1][k] + red[parity][3][k];
+            s[k] = a0 + a1;
         }
-        est[0] = est[0] + d[0];
-        est[1] = est[1] + d[1];
-        est[2] = est[2] + d[2];
+        float b[3] = {s[0], s[1], s[2]};
+        H[0] = s[3]; H[4] = s[4]; H[8] = s[5];
+        H[1] = s[6]; H[2] = s[7]; H[5] = s[8];
+        H[3] = H[1]; H[6] = H[2]; H[7] = H[5];
+        float clamp = 0.0f;
+        if ((H[0] != 0.0f) && (H[4] != 0.0f)) {
+            float d[3];
+            solve3(H, b, d);
+            if (d[2] > 0.2f) {
+                d[2] = 0.2f;
+                clamp = 1.0f;
+            } else if (d[2] < -0.2f) {
+                d[2] = -0.2f;
+                clamp = 1.0f;
+            }
+            est[0] = est[0] + d[0];
+            est[1] = est[1] + d[1];
+            est[2] = est[2] + d[2];
+        }
+        if ((tid & 63) == 0) {
+            sp[0] = est[0];
+            sp[1] = est[1];
+            sp[2] = est[2];
+            sp[3] = sdm_cosf(est[2]);
+            sp[4] = sdm_sinf(est[2]);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) sp[5 + k] = H[k];
+            sp[14] = clamp;
+        }
     }
+    __syncthreads();
+    est[0] = sp[0];
+    est[1] = sp[1];
+    est[2] = sp[2];
+    cs = sp[3];
+    sn = sp[4];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];
 }
 
 constexpr int MATCH_REG_PTS = 5;  // points per thread kept in registers: scans of up to 1280 points
@@ -435,6 +461,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     __shared__ unsigned nb_key[MATCH_REG_PTS * MATCH_THREADS];
     __shared__ float4 nb_val[MATCH_REG_PTS * MATCH_THREADS];
     __shared__ unsigned short mlist[MATCH_REG_PTS * MATCH_THREADS];  // per wave: slots whose cell moved
+    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity
     const int local = blockIdx.x;
     const int s = stream_begin + local;
     StreamState &st = state[s];
@@ -478,12 +505,15 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             map_from_world(g, tmp, est);
 #pragma unroll
             for (int j = 0; j < MATCH_REG_PTS; ++j) nb_key[threadIdx.x + j * MATCH_THREADS] = NB_NONE;  // own slots
+            float cs = sdm_cosf(est[2]), sn = sdm_sinf(est[2]);
             for (int it = 0; it <= iters; ++it) {
-                if (in_regs)
-                    gn_step_reg<MATCH_REG_PTS>(lc, g, preg, n, g.pts_scale, est, H, red, parity, &clamps, nb_key,
-                                               nb_val, mlist);
-                else
+                if (in_regs) {
+                    gn_step_reg<MATCH_REG_PTS>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, red, parity, nb_key,
+                                               nb_val, mlist, s_pose);
+                    clamps += s_pose[parity][14] != 0.0f ? 1 : 0;
+                } else {
                     gn_step(lc, g, pts, n, g.pts_scale, est, H, red, parity, &clamps);
+                }
                 parity ^= 1;
             }
             est[2] = normalize_angle(est[2]);

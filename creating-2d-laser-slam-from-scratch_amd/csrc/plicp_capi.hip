@@ -3,6 +3,8 @@
 // with PL_ENODEV.
 #include <hip/hip_runtime.h>
 
+#include <math.h>
+
 #include <string>
 #include <vector>
 
@@ -35,7 +37,7 @@ size_t pl_shmem(int n) { return (size_t)n * (sizeof(double2) + sizeof(unsigned l
 struct pl_ctx {
     int max_pairs = 0, max_rays = 0;
     pl_params params{};
-    double *d_ref = nullptr, *d_sens = nullptr, *d_guess = nullptr;
+    double *d_ref = nullptr, *d_sens = nullptr, *d_guess = nullptr, *d_theta = nullptr;
     pl_result *d_res = nullptr;
     hipStream_t stream = nullptr;
     bool timing = false;
@@ -89,6 +91,7 @@ int pl_create(pl_ctx **out, int max_pairs, int max_rays, const pl_params *params
     if ((e = hipMalloc(&c->d_ref, sizeof(double) * max_rays)) != hipSuccess ||
         (e = hipMalloc(&c->d_sens, sizeof(double) * max_rays)) != hipSuccess ||
         (e = hipMalloc(&c->d_guess, sizeof(double) * 3)) != hipSuccess ||
+        (e = hipMalloc(&c->d_theta, sizeof(double) * max_rays)) != hipSuccess ||
         (e = hipMalloc(&c->d_res, sizeof(pl_result))) != hipSuccess) {
         pl_destroy(c);
         return pfail(PL_ENOMEM, "hipMalloc", e);
@@ -104,6 +107,7 @@ int pl_destroy(pl_ctx *c)
     hipFree(c->d_ref);
     hipFree(c->d_sens);
     hipFree(c->d_guess);
+    hipFree(c->d_theta);
     hipFree(c->d_res);
     for (auto &p : c->ev_used) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
     for (auto &p : c->ev_free) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
@@ -113,7 +117,8 @@ int pl_destroy(pl_ctx *c)
 }
 
 static int pl_launch(pl_ctx *c, int count, int n, double angle_min, double angle_inc, const double *d_ref,
-                     const double *d_sens, const double *d_guess, pl_result *d_res, hipStream_t s)
+                     const double *d_sens, const double *d_guess, pl_result *d_res, hipStream_t s,
+                     const double *d_theta = nullptr)
 {
     if (count < 0 || count > c->max_pairs) return pfail(PL_EINVAL, "count exceeds max_pairs");
     if (n < 2 || n > c->max_rays) return pfail(PL_EINVAL, "n out of range");
@@ -135,7 +140,7 @@ static int pl_launch(pl_ctx *c, int count, int n, double angle_min, double angle
         auto kern = rpt <= 2 ? pl_icp_kernel<2> : rpt <= 4 ? pl_icp_kernel<4> : rpt <= 5 ? pl_icp_kernel<5>
                   : rpt <= 6 ? pl_icp_kernel<6> : pl_icp_kernel<PL_RPT_MAX>;
         hipLaunchKernelGGL(kern, dim3(count), dim3(PL_THREADS), pl_shmem(n), s, c->params, n, angle_min, angle_inc,
-                           d_ref, d_sens, d_guess, d_res);
+                           d_theta, d_ref, d_sens, d_guess, d_res);
     }
     PCHK(hipGetLastError());
     if (c->timing) {
@@ -155,6 +160,47 @@ int pl_icp(pl_ctx *c, int n, double angle_min, double angle_inc, const double *r
     PCHK(hipMemcpyAsync(c->d_sens, sens, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
     PCHK(hipMemcpyAsync(c->d_guess, first_guess ? first_guess : zero, sizeof(double) * 3, hipMemcpyHostToDevice, c->stream));
     int rc = pl_launch(c, 1, n, angle_min, angle_inc, c->d_ref, c->d_sens, c->d_guess, c->d_res, c->stream);
+    if (rc != PL_OK) return rc;
+    PCHK(hipMemcpyAsync(result, c->d_res, sizeof(pl_result), hipMemcpyDeviceToHost, c->stream));
+    PCHK(hipStreamSynchronize(c->stream));
+    return PL_OK;
+}
+
+int pl_set_params(pl_ctx *c, const pl_params *params)
+{
+    if (!c || !params) return pfail(PL_EINVAL, "NULL argument");
+    if (params->max_iterations < 1 || params->max_iterations > PL_MAX_IT)
+        return pfail(PL_EINVAL, "max_iterations must be in [1, 64]");
+    c->params = *params;
+    return PL_OK;
+}
+
+int pl_icp_ldp(pl_ctx *c, int n, const double *theta, const double *ref_readings, const int *ref_valid,
+               const double *sens_readings, const int *sens_valid, const double first_guess[3], pl_result *result)
+{
+    if (!c || !theta || !ref_readings || !sens_readings || !result) return pfail(PL_EINVAL, "NULL argument");
+    if (n < 2 || n > c->max_rays) return pfail(PL_EINVAL, "n out of range");
+    // the correspondence search maps polar angles to rays with the mean increment; an LDP of a
+    // LaserScan (angle_min + i * angle_increment, plicp_odometry.cc:306) is uniform to rounding
+    const double inc = (theta[n - 1] - theta[0]) / (double)(n - 1);
+    if (!(inc > 0.0)) return pfail(PL_EINVAL, "theta must increase");
+    for (int i = 0; i < n; ++i)
+        if (fabs(theta[i] - (theta[0] + i * inc)) > 1e-3 * inc)
+            return pfail(PL_EINVAL, "theta[] is not a uniform LaserScan grid");
+    // readings of invalid rays -> -1 (LaserScanToLDP, :297-301): valid[] decides, as ld_valid_ray does
+    std::vector<double> rr(ref_readings, ref_readings + n), sr(sens_readings, sens_readings + n);
+    for (int i = 0; i < n; ++i) {
+        if (ref_valid && !ref_valid[i]) rr[i] = -1.0;
+        if (sens_valid && !sens_valid[i]) sr[i] = -1.0;
+        if (!(rr[i] > 0.0)) rr[i] = -1.0;
+        if (!(sr[i] > 0.0)) sr[i] = -1.0;
+    }
+    const double zero[3] = {0.0, 0.0, 0.0};
+    PCHK(hipMemcpyAsync(c->d_ref, rr.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    PCHK(hipMemcpyAsync(c->d_sens, sr.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    PCHK(hipMemcpyAsync(c->d_theta, theta, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    PCHK(hipMemcpyAsync(c->d_guess, first_guess ? first_guess : zero, sizeof(double) * 3, hipMemcpyHostToDevice, c->stream));
+    int rc = pl_launch(c, 1, n, theta[0], inc, c->d_ref, c->d_sens, c->d_guess, c->d_res, c->stream, c->d_theta);
     if (rc != PL_OK) return rc;
     PCHK(hipMemcpyAsync(result, c->d_res, sizeof(pl_result), hipMemcpyDeviceToHost, c->stream));
     PCHK(hipStreamSynchronize(c->stream));

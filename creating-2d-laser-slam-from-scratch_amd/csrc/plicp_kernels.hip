@@ -199,8 +199,9 @@ __device__ __forceinline__ int pl_block_sum_int(int v, int *sred)
 // every instantiation -- only the register arrays shrink.
 template <int PL_RPT>
 __global__ void __launch_bounds__(PL_THREADS) __attribute__((amdgpu_waves_per_eu(PL_WAVES_PER_EU)))
-pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const double *__restrict__ ref_r,
-              const double *__restrict__ sens_r, const double *__restrict__ first_guess, pl_result *__restrict__ out)
+pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const double *__restrict__ theta,
+              const double *__restrict__ ref_r, const double *__restrict__ sens_r,
+              const double *__restrict__ first_guess, pl_result *__restrict__ out)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char pl_smem[];
     double2 *rpt = reinterpret_cast<double2 *>(pl_smem);                          // reference points [n]
@@ -226,7 +227,7 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
     // `dist > max_correspondence_dist^2` test skips them exactly like ld_valid_ray does.
     for (int i = tid; i < n; i += PL_THREADS) {
         const double r = rr[i];
-        const double th = angle_min + i * angle_inc;
+        const double th = theta ? theta[i] : angle_min + i * angle_inc;  // an LDP's own theta[] when given
         rpt[i] = r > 0.0 ? make_double2(r * sdm_cos(th), r * sdm_sin(th)) : make_double2(1e300, 1e300);
     }
     double spx[PL_RPT], spy[PL_RPT];
@@ -238,7 +239,7 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
         spx[k] = spy[k] = 0.0;
         if (i < n) {
             const double r = sr[i];
-            const double th = angle_min + i * angle_inc;
+            const double th = theta ? theta[i] : angle_min + i * angle_inc;
             sval[k] = r > 0.0;
             if (sval[k]) {
                 spx[k] = r * sdm_cos(th);
@@ -271,7 +272,8 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
     }
     __syncthreads();
 
-    const double min_theta = angle_min, max_theta = angle_min + (n - 1) * angle_inc;
+    // ldp->min_theta / max_theta = theta[0] / theta[n-1] (LaserScanToLDP, plicp_odometry.cc:312-313)
+    const double min_theta = theta ? theta[0] : angle_min, max_theta = theta ? theta[n - 1] : angle_min + (n - 1) * angle_inc;
     const double maxd2 = p.max_correspondence_dist * p.max_correspondence_dist;
     const int max_it = p.max_iterations < PL_MAX_IT ? p.max_iterations : PL_MAX_IT;
     double x_old[3], x_new[3];

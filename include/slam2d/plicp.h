@@ -74,6 +74,15 @@ int pl_icp_batch_device(pl_ctx *ctx, int count, int n, double angle_min, double 
                         const double *d_ref_readings, const double *d_sens_readings, const double *d_first_guess,
                         pl_result *d_results, void *hip_stream);
 
+/* Replace the context's parameters (sm_params fields, e.g. from the node's ROS params). */
+int pl_set_params(pl_ctx *ctx, const pl_params *params);
+/* sm_icp on two LDPs as lesson3 builds them (LaserScanToLDP, plicp_odometry.cc:285-322): shared theta[n]
+ * (uniform: angle_min + i * angle_increment, checked to 1e-3 of the increment), readings[n] and
+ * valid[n] (NULL = reading > 0) per scan; host arrays, synchronous.  The call include/slam2d/sm_icp_hip.h
+ * makes for its `slam2d_sm_icp(&input_, &output_)` drop-in of `sm_icp` (plicp_odometry.cc:391). */
+int pl_icp_ldp(pl_ctx *ctx, int n, const double *theta, const double *ref_readings, const int *ref_valid,
+               const double *sens_readings, const int *sens_valid, const double first_guess[3], pl_result *result);
+
 int pl_set_timing(pl_ctx *ctx, int enable);
 int pl_get_kernel_times(pl_ctx *ctx, double *ms_out, int64_t *launches_out, int reset);
 

@@ -54,11 +54,11 @@ typedef struct {
     int up[PLO_MAX_RAYS], down[PLO_MAX_RAYS];  /* next valid index above / below, -1 if none */
 } plo_scan;
 
-static void plo_cartesian(plo_scan *s, int n, double angle_min, double angle_inc, const double *r)
+static void plo_cartesian(plo_scan *s, int n, double angle_min, double angle_inc, const double *theta, const double *r)
 {
     s->n = n;
     for (int i = 0; i < n; ++i) {
-        const double th = angle_min + i * angle_inc;          /* LaserScanToLDP (plicp_odometry.cc:306) */
+        const double th = theta ? theta[i] : angle_min + i * angle_inc;  /* LaserScanToLDP (plicp_odometry.cc:306) */
         s->valid[i] = r[i] > 0.0;                              /* readings = -1 for invalid (:302) */
         s->px[i] = s->valid[i] ? r[i] * odm_cos(th) : 0.0;     /* ld_compute_cartesian */
         s->py[i] = s->valid[i] ? r[i] * odm_sin(th) : 0.0;
@@ -248,16 +248,17 @@ static double plo_kth(double *v, int k, int idx)  /* idx-th smallest of v[0..k) 
 }
 
 /* sm_icp for one scan pair; returns valid (all_is_okay).  info: iterations, nvalid; error. */
-int plo_icp(const plo_params *p, int n, double angle_min, double angle_inc, const double *ref_r, const double *sens_r,
-            const double *first_guess, int reduce_threads, double *x_out, int *iterations_out, int *nvalid_out,
-            double *error_out, int *trace_hashes)
+int plo_icp_theta(const plo_params *p, int n, double angle_min, double angle_inc, const double *theta,
+                  const double *ref_r, const double *sens_r, const double *first_guess, int reduce_threads,
+                  double *x_out, int *iterations_out, int *nvalid_out, double *error_out, int *trace_hashes)
 {
     if (n < 2 || n > PLO_MAX_RAYS) return 0;
     plo_scan *ref = (plo_scan *)malloc(sizeof(plo_scan));
     plo_scan *sens = (plo_scan *)malloc(sizeof(plo_scan));
-    plo_cartesian(ref, n, angle_min, angle_inc, ref_r);
-    plo_cartesian(sens, n, angle_min, angle_inc, sens_r);
-    const double min_theta = angle_min, max_theta = angle_min + (n - 1) * angle_inc;
+    plo_cartesian(ref, n, angle_min, angle_inc, theta, ref_r);
+    plo_cartesian(sens, n, angle_min, angle_inc, theta, sens_r);
+    /* ldp->min_theta / max_theta = theta[0] / theta[n-1] (LaserScanToLDP, plicp_odometry.cc:312-313) */
+    const double min_theta = theta ? theta[0] : angle_min, max_theta = theta ? theta[n - 1] : angle_min + (n - 1) * angle_inc;
     int *j1 = (int *)malloc(sizeof(int) * n), *j2 = (int *)malloc(sizeof(int) * n), *ok = (int *)malloc(sizeof(int) * n);
     double *d2 = (double *)malloc(sizeof(double) * n), *e = (double *)malloc(sizeof(double) * n);
     double *sorted = (double *)malloc(sizeof(double) * n), *best_j = (double *)malloc(sizeof(double) * n);
@@ -375,6 +376,15 @@ int plo_icp(const plo_params *p, int n, double angle_min, double angle_inc, cons
     if (error_out) *error_out = total_error;
     free(ref); free(sens); free(j1); free(j2); free(ok); free(d2); free(e); free(sorted); free(best_j); free(terms);
     return all_ok;
+}
+
+/* sm_icp with the uniform angles angle_min + i * angle_inc */
+int plo_icp(const plo_params *p, int n, double angle_min, double angle_inc, const double *ref_r, const double *sens_r,
+            const double *first_guess, int reduce_threads, double *x_out, int *iterations_out, int *nvalid_out,
+            double *error_out, int *trace_hashes)
+{
+    return plo_icp_theta(p, n, angle_min, angle_inc, NULL, ref_r, sens_r, first_guess, reduce_threads, x_out,
+                         iterations_out, nvalid_out, error_out, trace_hashes);
 }
 
 void plo_default_params(plo_params *p)

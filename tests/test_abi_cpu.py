@@ -12,7 +12,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 INC = os.path.join(REPO, "include", "slam2d")
 PKG_PY = os.path.join(REPO, "creating-2d-laser-slam-from-scratch_amd", "python", "slam2d")
 # C++ adapter headers of the ROS side (need the reference headers + Eigen), not part of the C-ABI
-CPP_ADAPTERS = {"MapRepHip.h"}
+CPP_ADAPTERS = {"MapRepHip.h", "sm_icp_hip.h"}
 C_HEADERS = sorted(f for f in os.listdir(INC) if f.endswith(".h") and f not in CPP_ADAPTERS)
 
 

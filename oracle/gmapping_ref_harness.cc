@@ -36,7 +36,8 @@ void gmr_map_size(double xmin, double ymin, double xmax, double ymax, double del
 }
 
 // One ComputeMap on a fresh map (gmapping.cc:135, :171-242).
-// Outputs are dense row-major [y*sx + x]:  n_out (hits), visits_out, acc_out (2 floats per cell).
+// Outputs are dense row-major [y*sx + x]:  n_out (hits), visits_out, acc_out (2 floats per cell), any
+// may be NULL (all NULL: ComputeMap alone, as bench.py times the reference's CPU path).
 // Returns the number of free-cell updates (Σ (num_points-1)).
 long long gmr_compute_map(double px, double py, double ct, double st,
                           const float *ranges, int nbeams, const double *a_cos, const double *a_sin,
@@ -90,6 +91,7 @@ long long gmr_compute_map(double px, double py, double ct, double st,
         map.cell(p1).update(true, hit);
     }
     *num_hits = (int)hit_lists.size();
+    if (!n_out && !visits_out && !acc_out) return nfree;  // ComputeMap only (CPU-baseline timing)
     int sx = map.getMapSizeX(), sy = map.getMapSizeY();
     const ScanMatcherMap &cm = map;
     for (int y = 0; y < sy; y++) {
@@ -97,8 +99,8 @@ long long gmr_compute_map(double px, double py, double ct, double st,
             IntPoint p(x, y);
             const PointAccumulator &c = cm.cell(p);
             size_t o = (size_t)y * sx + x;
-            n_out[o] = c.n;
-            visits_out[o] = c.visits;
+            if (n_out) n_out[o] = c.n;
+            if (visits_out) visits_out[o] = c.visits;
             if (acc_out) {
                 acc_out[2 * o] = c.acc.x;
                 acc_out[2 * o + 1] = c.acc.y;

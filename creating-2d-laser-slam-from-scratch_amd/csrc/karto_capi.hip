@@ -225,10 +225,18 @@ int kt_chunk_build(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, 
 int kt_chunk_coarse(kt_ctx *c, int count, int pass, int penalize, int shard, int nshards, hipStream_t s)
 {
     const KtGeom &g = c->g;
-    const long long blocks = (long long)((count + 7) / 8) * 8 * g.nang[pass] * g.tiles * g.tiles;
+    // angles per workgroup: 1 (r02 A/B, loop window / sequential batch: 7 angles 5 % / 3 angles 5 % slower,
+    // 21 angles 29 % slower -- fewer workgroups left in flight for the gathers); SLAM2D_KT_AG overrides
+    const long long per_angle = (long long)((count + 7) / 8) * 8 * g.tiles * g.tiles;
+    const int nA = g.nang[pass];
+    long long ag = 1;
+    if (const char *e = getenv("SLAM2D_KT_AG")) ag = atoll(e);
+    ag = ag < 1 ? 1 : (ag > nA ? nA : ag);
+    const long long blocks = per_angle * ((nA + ag - 1) / ag);
     if (blocks > 0x7fffffffLL) return kfail(KT_EINVAL, "coarse launch too large: lower the batch size");
     KT_LAUNCH(K_COARSE, kt_coarse_kernel, dim3((unsigned)blocks), dim3(KT_THREADS), (size_t)g.n * sizeof(int), s, g,
-              c->pool(), c->d_state, c->d_grids, c->d_resp, c->d_posmax, count, pass, penalize, shard, nshards);
+              c->pool(), c->d_state, c->d_grids, c->d_resp, c->d_posmax, count, pass, penalize, shard, nshards,
+              (int)ag);
     return KT_OK;
 }
 

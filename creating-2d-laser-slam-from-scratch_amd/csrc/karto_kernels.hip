@@ -14,7 +14,7 @@
 //                      smear kernel: chunks of 16 consecutive points rendered in an LDS tile, merged
 //                      into the grid by 64-bit compare-and-swap per non-zero qword.  Order-free because
 //                      the kernel's only 100 is its centre (checked at kt_create).
-//   kt_coarse_kernel   per (match, angle, 16x16 position tile): GridIndexLookup::ComputeOffsets for one
+//   kt_coarse_kernel   per (match, group of angles, 16x16 position tile): GridIndexLookup::ComputeOffsets per
 //                      angle into LDS (Karto.h:6455-6501), then GetResponse (Mapper.cpp:819-856) for the
 //                      tile's 256 positions -- each lane owns 4 positions two cells apart and reads
 //                      them with ONE unaligned 8-byte gather per point (bytes 0, 2, 4, 6), summed as
@@ -775,11 +775,21 @@ kt_clear_tiles_kernel(KtGeom g, unsigned char *grids, const int *__restrict__ di
 }
 
 // =================================================================================================
-// kt_coarse_kernel: GetResponse over a 16x16 tile of positions for one angle
+// kt_coarse_kernel: GetResponse over a 16x16 tile of positions for a group of `ag` consecutive angles
+//
+// The workgroup keeps its positions and walks its angles: per angle the query's offsets
+// (GridIndexLookup::ComputeOffsets) into LDS, the gathers, the responses.  A position's `ag` responses
+// are stored angle-major (resp[a * npos + pos], the select kernel reads them back in the reference's
+// pose order pos * nA + a), so each angle's 256 responses leave as one contiguous 2 KB run: stored
+// position-major, each workgroup wrote 8-byte pieces 8 * nA bytes apart and the launch wrote 157 MB for
+// 55 MB of responses (r01el, r02ae).  The per-position maximum over the group's angles is kept in a
+// register for the match's best response only: the per-position maximum over all angles is derived
+// from the stored responses by kt_select_kernel (no 64-bit atomic per position and angle).  ag = 1 by
+// default (grouping measured slower: fewer workgroups in flight for the gathers); SLAM2D_KT_AG sets it.
 // =================================================================================================
 __global__ void __launch_bounds__(KT_THREADS)
 kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict__ grids, double *resp,
-                 unsigned long long *posmax, int count, int pass, int penalize, int shard, int nshards)
+                 unsigned long long *posmax, int count, int pass, int penalize, int shard, int nshards, int ag)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char kt_smem[];
     int *soff = reinterpret_cast<int *>(kt_smem);  // [npts]
@@ -787,8 +797,9 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
     __shared__ double sbest[4];
 
     const int nA = g.nang[pass];
+    const int ngrp = (nA + ag - 1) / ag;
     const int T2 = g.tiles * g.tiles;
-    const int W = nA * T2;
+    const int W = ngrp * T2;
     // XCD-aware: all work of one match runs on one XCD (blocks are dealt round-robin to the 8 XCDs)
     const int b = blockIdx.x;
     const int xcd = b & 7, q8 = b >> 3;
@@ -797,34 +808,19 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
     if (m >= count) return;
     KtState &S = st[m];
     if (S.pass != pass) return;
-    const int a = w / T2, t = w - a * T2;
+    const int agrp = w / T2, t = w - agrp * T2;
+    const int a0 = agrp * ag, a1 = min(a0 + ag, nA);
     const int ty = t / g.tiles, tx = t - ty * g.tiles;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // window sharded over GPUs (kt_match_sharded_begin_device): this rank owns the angles
-    // a = shard (mod nshards); the others' responses are left +0.0 for the MAX all-reduce
-    const bool owned = (a % nshards) == shard;
 
     const double cxs = S.center[0], cys = S.center[1], chs = S.center[2];
     const double gox = S.gox, goy = S.goy;
     const double aoff = g.aoff[pass];
     const double start = chs - aoff;
-    const double angle = start + (double)(uint32_t)a * g.cares;
-    const double cs = sdm_cos(angle), sn = sdm_sin(angle);
     const int q = S.query, npts = S.npts;
     const double2 *loc = P.loc + (size_t)q * g.n;
     const unsigned char *bad = P.bad + (size_t)q * g.n;
-    for (int k = tid; owned && k < npts; k += KT_THREADS) {
-        int o = KT_INVALID;
-        if (!bad[k]) {
-            const double2 l = loc[k];
-            const double ox = cs * l.x - sn * l.y;
-            const double oy = sn * l.x + cs * l.y;
-            const int gx = kt_w2g(ox + gox, gox, g.scale), gy = kt_w2g(oy + goy, goy, g.scale);
-            o = gx + gy * g.ws;
-        }
-        soff[k] = o;
-    }
-    // this lane's 4 positions: row iy, columns ix0 .. ix0 + 3
+    // this lane's 4 gather positions: row iy, columns ix0 .. ix0 + 3
     const int iy = ty * KT_TILE + (lane >> 2);
     const int ix0 = tx * KT_TILE + (lane & 3) * 4;
     const double startX = -g.coff;
@@ -849,113 +845,134 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
             }
         }
     }
-    if (!owned) {  // block-uniform
-        const int pl = tid >> 2, pj = tid & 3;
-        const int piy = ty * KT_TILE + (pl >> 2);
-        const int pix = tx * KT_TILE + (pl & 3) * 4 + pj;
-        if (piy < g.nxy && pix < g.nxy) resp[(size_t)m * g.max_poses + ((size_t)piy * g.nxy + pix) * nA + a] = 0.0;
-        return;
-    }
-    __syncthreads();
-    const unsigned ds = (unsigned)g.data_size;
-    const unsigned lim = ds - 6u;
-    const unsigned char *grid = grids + (size_t)m * g.grid_stride;
-    unsigned c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    unsigned acc01 = 0, acc23 = 0;
-    int since = 0;
-    if (fast) {
-        // 8 points per iteration: 8 independent 8-byte gathers in flight per lane
-        const int base = gpos[0];
-        int k = wave;
-        for (; k + 28 < npts; k += 32) {
-            int bi[8];
-            bool allin = true;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                bi[j] = base + soff[k + 4 * j];
-                allin = allin && (unsigned)bi[j] < lim;
-            }
-            if (allin) {
-                uint2 v[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) __builtin_memcpy(&v[j], grid + bi[j], 8);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    acc01 += v[j].x & 0x00FF00FFu;
-                    acc23 += v[j].y & 0x00FF00FFu;
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int b = bi[j];
-                    if ((unsigned)b < ds) c0 += grid[b];
-                    if ((unsigned)(b + 2) < ds) c1 += grid[b + 2];
-                    if ((unsigned)(b + 4) < ds) c2 += grid[b + 4];
-                    if ((unsigned)(b + 6) < ds) c3 += grid[b + 6];
-                }
-            }
-            since += 8;
-            if (since >= 504) {  // 512 * 100 < 65536: flush the packed 16-bit sums
-                c0 += acc01 & 0xFFFFu; c1 += acc01 >> 16; c2 += acc23 & 0xFFFFu; c3 += acc23 >> 16;
-                acc01 = acc23 = 0;
-                since = 0;
-            }
-        }
-        for (; k < npts; k += 4) {
-            const int bi = base + soff[k];
-            if ((unsigned)bi < lim) {
-                uint2 v;
-                __builtin_memcpy(&v, grid + bi, 8);
-                acc01 += v.x & 0x00FF00FFu;
-                acc23 += v.y & 0x00FF00FFu;
-            } else {
-                if ((unsigned)bi < ds) c0 += grid[bi];
-                if ((unsigned)(bi + 2) < ds) c1 += grid[bi + 2];
-                if ((unsigned)(bi + 4) < ds) c2 += grid[bi + 4];
-                if ((unsigned)(bi + 6) < ds) c3 += grid[bi + 6];
-            }
-        }
-        c0 += acc01 & 0xFFFFu; c1 += acc01 >> 16; c2 += acc23 & 0xFFFFu; c3 += acc23 >> 16;
-    } else {
-        for (int k = wave; k < npts; k += 4) {
-            const int o = soff[k];
-            const int i0 = gpos[0] + o, i1 = gpos[1] + o, i2 = gpos[2] + o, i3 = gpos[3] + o;
-            if ((unsigned)i0 < ds) c0 += grid[i0];
-            if ((unsigned)i1 < ds) c1 += grid[i1];
-            if ((unsigned)i2 < ds) c2 += grid[i2];
-            if ((unsigned)i3 < ds) c3 += grid[i3];
-        }
-    }
-    scnt[wave][lane * 4 + 0] = c0;
-    scnt[wave][lane * 4 + 1] = c1;
-    scnt[wave][lane * 4 + 2] = c2;
-    scnt[wave][lane * 4 + 3] = c3;
-    __syncthreads();
-    // one thread per position of the tile
-    const unsigned total = scnt[0][tid] + scnt[1][tid] + scnt[2][tid] + scnt[3][tid];
+    // the position this thread finalises (one per thread of the tile)
     const int pl = tid >> 2, pj = tid & 3;
     const int piy = ty * KT_TILE + (pl >> 2);
     const int pix = tx * KT_TILE + (pl & 3) * 4 + pj;
-    double best = 0.0;
-    if (piy < g.nxy && pix < g.nxy) {
-        double response = 0.0;
-        if (npts > 0) response = (double)total / (double)(uint32_t)(npts * KT_OCC);
-        if (penalize && !kt_deq(response, 0.0)) {
-            const double x = startX + (double)(uint32_t)pix * g.cres;
-            const double y = startX + (double)(uint32_t)piy * g.cres;
-            const double sqd = kt_sq(x) + kt_sq(y);
-            double dp = 1.0 - (KT_GAIN * sqd / g.dvp);
-            dp = kt_max(dp, g.mdp);
-            const double sqa = kt_sq(angle - chs);
-            double ap = 1.0 - (KT_GAIN * sqa / g.avp);
-            ap = kt_max(ap, g.map_);
-            response *= (dp * ap);
+    const bool pin = piy < g.nxy && pix < g.nxy;
+    const size_t pos = (size_t)piy * g.nxy + pix;
+    // responses angle-major (resp[a * npos + pos]): a workgroup's 256 positions are one contiguous 2 KB run
+    const size_t npos = (size_t)g.nxy * g.nxy;
+    double *rpos = resp + (size_t)m * g.max_poses + pos;
+    double pmax = 0.0;   // max over this group's angles at this position (responses are >= 0)
+
+    const unsigned ds = (unsigned)g.data_size;
+    const unsigned lim = ds - 6u;
+    const unsigned char *grid = grids + (size_t)m * g.grid_stride;
+    for (int a = a0; a < a1; ++a) {
+        // window sharded over GPUs (kt_match_sharded_begin_device): this rank owns the angles
+        // a = shard (mod nshards); the others' responses are left +0.0 for the MAX all-reduce
+        if ((a % nshards) != shard) {  // block-uniform
+            if (pin) rpos[(size_t)a * npos] = 0.0;
+            continue;
         }
-        const size_t pos = (size_t)piy * g.nxy + pix;
-        resp[(size_t)m * g.max_poses + pos * nA + a] = response;
-        atomicMax(posmax + (size_t)m * g.nxy * g.nxy + pos, kt_bits(response));
-        best = response;
+        const double angle = start + (double)(uint32_t)a * g.cares;
+        const double cs = sdm_cos(angle), sn = sdm_sin(angle);
+        __syncthreads();  // the previous angle's offsets are no longer read
+        for (int k = tid; k < npts; k += KT_THREADS) {
+            int o = KT_INVALID;
+            if (!bad[k]) {
+                const double2 l = loc[k];
+                const double ox = cs * l.x - sn * l.y;
+                const double oy = sn * l.x + cs * l.y;
+                const int gx = kt_w2g(ox + gox, gox, g.scale), gy = kt_w2g(oy + goy, goy, g.scale);
+                o = gx + gy * g.ws;
+            }
+            soff[k] = o;
+        }
+        __syncthreads();
+        unsigned c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        unsigned acc01 = 0, acc23 = 0;
+        int since = 0;
+        if (fast) {
+            // 8 points per iteration: 8 independent 8-byte gathers in flight per lane
+            const int base = gpos[0];
+            int k = wave;
+            for (; k + 28 < npts; k += 32) {
+                int bi[8];
+                bool allin = true;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    bi[j] = base + soff[k + 4 * j];
+                    allin = allin && (unsigned)bi[j] < lim;
+                }
+                if (allin) {
+                    uint2 v[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) __builtin_memcpy(&v[j], grid + bi[j], 8);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        acc01 += v[j].x & 0x00FF00FFu;
+                        acc23 += v[j].y & 0x00FF00FFu;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int b = bi[j];
+                        if ((unsigned)b < ds) c0 += grid[b];
+                        if ((unsigned)(b + 2) < ds) c1 += grid[b + 2];
+                        if ((unsigned)(b + 4) < ds) c2 += grid[b + 4];
+                        if ((unsigned)(b + 6) < ds) c3 += grid[b + 6];
+                    }
+                }
+                since += 8;
+                if (since >= 504) {  // 512 * 100 < 65536: flush the packed 16-bit sums
+                    c0 += acc01 & 0xFFFFu; c1 += acc01 >> 16; c2 += acc23 & 0xFFFFu; c3 += acc23 >> 16;
+                    acc01 = acc23 = 0;
+                    since = 0;
+                }
+            }
+            for (; k < npts; k += 4) {
+                const int bi = base + soff[k];
+                if ((unsigned)bi < lim) {
+                    uint2 v;
+                    __builtin_memcpy(&v, grid + bi, 8);
+                    acc01 += v.x & 0x00FF00FFu;
+                    acc23 += v.y & 0x00FF00FFu;
+                } else {
+                    if ((unsigned)bi < ds) c0 += grid[bi];
+                    if ((unsigned)(bi + 2) < ds) c1 += grid[bi + 2];
+                    if ((unsigned)(bi + 4) < ds) c2 += grid[bi + 4];
+                    if ((unsigned)(bi + 6) < ds) c3 += grid[bi + 6];
+                }
+            }
+            c0 += acc01 & 0xFFFFu; c1 += acc01 >> 16; c2 += acc23 & 0xFFFFu; c3 += acc23 >> 16;
+        } else {
+            for (int k = wave; k < npts; k += 4) {
+                const int o = soff[k];
+                const int i0 = gpos[0] + o, i1 = gpos[1] + o, i2 = gpos[2] + o, i3 = gpos[3] + o;
+                if ((unsigned)i0 < ds) c0 += grid[i0];
+                if ((unsigned)i1 < ds) c1 += grid[i1];
+                if ((unsigned)i2 < ds) c2 += grid[i2];
+                if ((unsigned)i3 < ds) c3 += grid[i3];
+            }
+        }
+        scnt[wave][lane * 4 + 0] = c0;
+        scnt[wave][lane * 4 + 1] = c1;
+        scnt[wave][lane * 4 + 2] = c2;
+        scnt[wave][lane * 4 + 3] = c3;
+        __syncthreads();
+        // one thread per position of the tile
+        const unsigned total = scnt[0][tid] + scnt[1][tid] + scnt[2][tid] + scnt[3][tid];
+        if (pin) {
+            double response = 0.0;
+            if (npts > 0) response = (double)total / (double)(uint32_t)(npts * KT_OCC);
+            if (penalize && !kt_deq(response, 0.0)) {
+                const double x = startX + (double)(uint32_t)pix * g.cres;
+                const double y = startX + (double)(uint32_t)piy * g.cres;
+                const double sqd = kt_sq(x) + kt_sq(y);
+                double dp = 1.0 - (KT_GAIN * sqd / g.dvp);
+                dp = kt_max(dp, g.mdp);
+                const double sqa = kt_sq(angle - chs);
+                double ap = 1.0 - (KT_GAIN * sqa / g.avp);
+                ap = kt_max(ap, g.map_);
+                response *= (dp * ap);
+            }
+            rpos[(size_t)a * npos] = response;
+            pmax = kt_max(pmax, response);
+        }
     }
+    double best = pmax;  // posmax itself is taken from the stored responses by kt_select_kernel
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) best = kt_max(best, __shfl_xor(best, off, 64));
     if (lane == 0) sbest[wave] = best;
@@ -1030,27 +1047,35 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
         s_err = 0;
     }
     __syncthreads();
-    // poses with DoubleEqual(response, best), in pose order (16 consecutive poses per thread and pass)
-    for (int base = 0; base < np; base += KT_THREADS * KT_SEL_ITEMS) {
-        const int i0 = base + tid * KT_SEL_ITEMS;
-        unsigned fl = 0;
+    // Poses with DoubleEqual(response, best), in the reference's pose order i = pos * nA + a, and the
+    // per-position maximum over the angles (the search-space probability grid, posmax).  kt_coarse_kernel
+    // stores the responses angle-major, so thread tid takes position base + tid and walks its angles
+    // (coalesced across the threads); ordering the ties by thread within a round keeps pose order.
+    const int npos = nxy * nxy;
+    unsigned long long *pmw = posmax + (size_t)m * npos;
+    for (int base = 0; base < npos; base += KT_THREADS) {
+        const int pos = base + tid;
         int c = 0;
+        double mx = 0.0;
+        if (pos < npos)
+            for (int a0 = 0; a0 < nA; a0 += 8) {  // 8 independent loads in flight per thread
+                double v[8];
 #pragma unroll
-        for (int j = 0; j < KT_SEL_ITEMS; ++j) {
-            const int i = i0 + j;
-            if (i < np && kt_deq(r[i], best)) {
-                fl |= 1u << j;
-                ++c;
+                for (int j = 0; j < 8; ++j) v[j] = a0 + j < nA ? r[(size_t)(a0 + j) * npos + pos] : 0.0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (a0 + j < nA) {
+                        mx = kt_max(mx, v[j]);
+                        c += kt_deq(v[j], best) ? 1 : 0;
+                    }
             }
-        }
+        if (pos < npos) pmw[pos] = kt_bits(mx);
         int tot;
         int pre = kt_block_exscan(c, sw, &tot);
         const int n0 = s_n;
-        while (fl) {
-            const int j = __builtin_ctz(fl);
-            fl &= fl - 1;
-            ti[n0 + pre++] = i0 + j;
-        }
+        if (c)
+            for (int a = 0; a < nA; ++a)
+                if (kt_deq(r[(size_t)a * npos + pos], best)) ti[n0 + pre++] = pos * nA + a;
         __syncthreads();
         if (tid == 0) s_n = n0 + tot;
         __syncthreads();

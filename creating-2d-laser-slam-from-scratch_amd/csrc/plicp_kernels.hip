@@ -96,12 +96,22 @@ __device__ __forceinline__ void pl_terms(double px, double py, double qx, double
     o[13] = -2.0 * (-py * a0 + px * a1);
 }
 
-// constrained point-to-line solve (the role of CSM's gpc_solve); false if degenerate
-__device__ __attribute__((noinline)) bool pl_gpc_solve(const double *m, double *x)
+// constrained point-to-line solve (the role of CSM's gpc_solve); false if degenerate.  It reads the 14
+// GPC sums as the 4 waves' partial sums in LDS (red[w][k], combined in pl_block_sum's order) and leaves
+// its estimate in LDS x[3]: out of line (the bisection's registers stay out of the kernel's budget) with
+// no array argument in private memory, so a call costs no scratch traffic.
+__device__ __forceinline__ double pl_red_sum(const double (*red)[16], int k)
 {
-    const double m00 = m[0], m01 = m[1], m02 = m[2], m03 = m[3], m11 = m[4], m12 = m[5], m13 = m[6];
-    const double m22 = m[7], m23 = m[8], m33 = m[9];
-    const double g0 = m[10], g1 = m[11], g2 = m[12], g3 = m[13];
+    return (red[0][k] + red[2][k]) + (red[1][k] + red[3][k]);
+}
+__device__ __attribute__((noinline)) bool pl_gpc_solve(const double (*red)[16], double *x)
+{
+    const double m00 = pl_red_sum(red, 0), m01 = pl_red_sum(red, 1), m02 = pl_red_sum(red, 2);
+    const double m03 = pl_red_sum(red, 3), m11 = pl_red_sum(red, 4), m12 = pl_red_sum(red, 5);
+    const double m13 = pl_red_sum(red, 6), m22 = pl_red_sum(red, 7), m23 = pl_red_sum(red, 8);
+    const double m33 = pl_red_sum(red, 9);
+    const double g0 = pl_red_sum(red, 10), g1 = pl_red_sum(red, 11), g2 = pl_red_sum(red, 12);
+    const double g3 = pl_red_sum(red, 13);
     const double detA = m00 * m11 - m01 * m01;
     if (!(detA > 0.0)) return false;
     const double ia00 = m11 / detA, ia01 = -m01 / detA, ia11 = m00 / detA;
@@ -161,8 +171,17 @@ __device__ __forceinline__ double pl_angle_diff(double a, double b)
 
 // block-wide sums (xor butterfly inside each wave, then ((w0 + w2) + (w1 + w3)) -- the oracle's
 // reduce_threads = 256 order)
+// a block-uniform double moved to scalar registers (the pose estimates: kept out of the VGPR budget)
+__device__ __forceinline__ double pl_uniform(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(unsigned)(unsigned long long)b);
+    const int hi = __builtin_amdgcn_readfirstlane((int)((unsigned long long)b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+// the wave half: each wave's sums into red[w][*] (no barrier)
 template <int K>
-__device__ __forceinline__ void pl_block_sum(double *v, double (*red)[16])
+__device__ __forceinline__ void pl_wave_sums(double *v, double (*red)[16])
 {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1)
@@ -172,9 +191,14 @@ __device__ __forceinline__ void pl_block_sum(double *v, double (*red)[16])
     if ((threadIdx.x & 63) == 0)
 #pragma unroll
         for (int k = 0; k < K; ++k) red[w][k] = v[k];
+}
+template <int K>
+__device__ __forceinline__ void pl_block_sum(double *v, double (*red)[16])
+{
+    pl_wave_sums<K>(v, red);
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = (red[0][k] + red[2][k]) + (red[1][k] + red[3][k]);
+    for (int k = 0; k < K; ++k) v[k] = pl_red_sum(red, k);
     __syncthreads();
 }
 
@@ -287,6 +311,11 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
     x_new[0] = x_old[0];
     x_new[1] = x_old[1];
     x_new[2] = x_old[2];
+    if (tid == 0) {  // the solve's in/out estimate lives in LDS (read back after the barriers below)
+        s_x[0] = x_new[0];
+        s_x[1] = x_new[1];
+        s_x[2] = x_new[2];
+    }
     bool all_ok = true;
     int it = 0, nvalid = 0;
     double total_error = 0.0;
@@ -555,30 +584,27 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
 #pragma unroll
             for (int q = 0; q < 14; ++q) m[q] = m[q] + t[q];
         }
-        pl_block_sum<14>(m, red);
+        pl_wave_sums<14>(m, red);
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) hsum += __shfl_xor(hsum, off, 64);
         if ((tid & 63) == 0) sred[tid >> 6] = (int)hsum;
         __syncthreads();
         // the solve's barrier below separates this read from the next write of sred
         const unsigned hash = ((unsigned)sred[0] + (unsigned)sred[1] + (unsigned)sred[2] + (unsigned)sred[3]) & 0x7FFFFFFFu;
-        // the constrained solve once per pair (wave 0), broadcast: on failure x_new keeps what
-        // pl_gpc_solve left in it, as in the all-threads version
+        // the constrained solve once per pair (wave 0) on the waves' sums in red, its estimate left in
+        // s_x (= x_new on entry): on failure x_new keeps what pl_gpc_solve left there, as in the
+        // all-threads version
         if (tid < 64) {
-            double xs[3] = {x_new[0], x_new[1], x_new[2]};
-            const bool okk = pl_gpc_solve(m, xs);
+            const bool okk = pl_gpc_solve(red, s_x);
             if (tid == 0) {
                 s_hash[it] = hash;
-                s_x[0] = xs[0];
-                s_x[1] = xs[1];
-                s_x[2] = xs[2];
                 s_ok = okk ? 1 : 0;
             }
         }
         __syncthreads();
-        x_new[0] = s_x[0];
-        x_new[1] = s_x[1];
-        x_new[2] = s_x[2];
+        x_new[0] = pl_uniform(s_x[0]);
+        x_new[1] = pl_uniform(s_x[1]);
+        x_new[2] = pl_uniform(s_x[2]);
         if (!s_ok) {
             all_ok = false;
             break;

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 cd /tmp
 for spec in "$@"; do
   for ctr in WRITE_SIZE FETCH_SIZE; do
-    OUT=$ROOT/gpurun_out/pmcw_${TAG}_$(echo "$spec" | tr '=,' '__')_$ctr
+    OUT=$ROOT/gpurun_out/pmcw_${TAG}_$(echo "$spec" | tr '=,/' '___' | tail -c 60)_$ctr
     env $spec timeout -k 10 120 rocprofv3 --pmc $ctr -d "$OUT" -o run --output-format csv -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-copy-probe --steps 3 --warmup 1 $ARGS > "$OUT.log" 2>&1 || { echo "FAIL $spec $ctr"; exit 1; }
     python3 - "$OUT" "$KER" "$spec" "$ctr" <<'PY'
 import csv, glob, sys

@@ -96,6 +96,7 @@ struct hs_ctx {
     // half's match.  Measured slower at the north-star size (0.97 M vs 1.04 M scans/s: the update
     // kernel already fills the CUs, and a concurrent match slows it more than it hides), so off by default.
     bool pipeline = false;
+    bool fuse_ingest = true;  // range arrays: ingest inside the match kernel (SLAM2D_FUSE_INGEST=0: own kernel)
     hipEvent_t ev_upd[MAX_PARTS] = {};
     // the last device work of the context (every *_device call waits for it on its own stream, so the
     // per-context scratch -- update lists, ingest buffers, queues -- is never used by two streams at once)
@@ -215,7 +216,7 @@ void end_timed(hs_ctx *c, hipStream_t s)
 
 int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int xy_stride, const int *n,
                 const float2 *origo, const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s,
-                hipEvent_t wait_before_update = nullptr)
+                hipEvent_t wait_before_update = nullptr, const MatchIngest *mi = nullptr)
 {
     WorkQueue *wq = c->d_wq + part;
     uint4 *segs = c->d_segs + (size_t)part * c->seg_cap;
@@ -229,7 +230,8 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     UpdList *wl_cur = use_list ? c->wl[part][c->wl_parity[part]] : nullptr;
     begin_timed(c, 0, s);
     hipLaunchKernelGGL(hs_match_kernel, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state, xy,
-                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur);
+                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur, c->ingest,
+                       mi ? *mi : MatchIngest{});
     end_timed(c, s);
     HCHK(hipGetLastError());
     if (mode == MODE_MATCH_ONLY) return HS_OK;
@@ -293,11 +295,13 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
 }
 
 int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride, const int *n, const float2 *origo,
-                const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s)
+                const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s,
+                const MatchIngest *mi = nullptr)
 {
     if (count <= 0) return HS_OK;
     const int parts = (mode == MODE_PROCESS && count >= 64 * c->nparts) ? c->nparts : 1;
-    if (parts == 1) return launch_part(c, 0, begin, count, xy, xy_stride, n, origo, hints, mode, out_pose, out_cov, s);
+    if (parts == 1)
+        return launch_part(c, 0, begin, count, xy, xy_stride, n, origo, hints, mode, out_pose, out_cov, s, nullptr, mi);
     HCHK(hipEventRecord(c->ev_start, s));
     const int per = (count + parts - 1) / parts;
     for (int p = 0; p < parts; ++p) {
@@ -306,10 +310,17 @@ int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride
         if (cnt <= 0) break;
         hipStream_t ps = c->pstream[p];
         HCHK(hipStreamWaitEvent(ps, c->ev_start, 0));
+        MatchIngest pmi = mi ? *mi : MatchIngest{};
+        if (mi) {
+            pmi.ranges += (size_t)off * mi->rstride;
+            pmi.xy_out += (size_t)off * xy_stride;
+            pmi.n_out += off;
+            pmi.origo_out += off;
+        }
         int rc = launch_part(c, p, begin + off, cnt, xy + (size_t)off * xy_stride, xy_stride, n + off,
                              origo ? origo + off : nullptr, hints ? hints + 3 * (size_t)off : nullptr, mode,
                              out_pose ? out_pose + 3 * (size_t)off : nullptr, out_cov ? out_cov + 9 * (size_t)off : nullptr,
-                             ps);
+                             ps, nullptr, mi ? &pmi : nullptr);
         if (rc != HS_OK) return rc;
         HCHK(hipEventRecord(c->ev_done[p], ps));
         HCHK(hipStreamWaitEvent(s, c->ev_done[p], 0));
@@ -347,6 +358,21 @@ int launch_ingest(hs_ctx *c, int count, const float *d_ranges, int range_stride,
                        xy_stride, d_n, d_origo);
     HCHK(hipGetLastError());
     return HS_OK;
+}
+
+// ingest + step on range arrays: the ingest runs inside the match kernel (one launch less) when the
+// scan fits the match kernel's registers (<= 1280 beams) unless SLAM2D_FUSE_INGEST=0; else its own kernel.
+int launch_ranges_step(hs_ctx *c, int begin, int count, const float *d_ranges, int range_stride, float2 *xy,
+                       int xy_stride, int *d_n, float2 *d_origo, const float *hints, float *out_pose, float *out_cov,
+                       hipStream_t s)
+{
+    if (c->fuse_ingest && c->ingest.n <= MATCH_THREADS * MATCH_REG_PTS) {
+        const MatchIngest mi{d_ranges, range_stride, c->d_cs, xy, d_n, d_origo};
+        return launch_step(c, begin, count, xy, xy_stride, d_n, d_origo, hints, MODE_PROCESS, out_pose, out_cov, s, &mi);
+    }
+    int rc = launch_ingest(c, count, d_ranges, range_stride, xy, xy_stride, d_n, d_origo, s);
+    if (rc == HS_OK) rc = launch_step(c, begin, count, xy, xy_stride, d_n, d_origo, hints, MODE_PROCESS, out_pose, out_cov, s);
+    return rc;
 }
 
 // Stage one host scan into the single-stream buffers.
@@ -434,6 +460,8 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         c->tile_grid = ncu * (tg ? atoi(tg) : per_cu);
         const char *pp = getenv("SLAM2D_PIPELINE");
         c->pipeline = pp && atoi(pp) != 0;
+        const char *fi = getenv("SLAM2D_FUSE_INGEST");
+        c->fuse_ingest = !(fi && atoi(fi) == 0);
         const char *np = getenv("SLAM2D_PARTS");
         c->nparts = np ? atoi(np) : 1;
         const char *um = getenv("SLAM2D_UPDATE");
@@ -765,13 +793,9 @@ int hs_run_ranges_device(hs_ctx *c, int steps, const float *d_ranges, int range_
     int rc = dev_enter(c, s);
     if (rc != HS_OK) return rc;
     if (!pipeline_ok(c)) {  // default: the steps in order on s
-        for (int k = 0; k < steps && rc == HS_OK; ++k) {
-            rc = launch_ingest(c, c->B, d_ranges + (size_t)k * step_stride, range_stride, c->d_ixy, c->max_points, c->d_in,
-                               c->d_iorigo, s);
-            if (rc == HS_OK)
-                rc = launch_step(c, 0, c->B, c->d_ixy, c->max_points, c->d_in, c->d_iorigo, nullptr, MODE_PROCESS, nullptr,
-                                 nullptr, s);
-        }
+        for (int k = 0; k < steps && rc == HS_OK; ++k)
+            rc = launch_ranges_step(c, 0, c->B, d_ranges + (size_t)k * step_stride, range_stride, c->d_ixy, c->max_points,
+                                    c->d_in, c->d_iorigo, nullptr, nullptr, nullptr, s);
         return rc == HS_OK ? dev_leave(c, s) : rc;
     }
     // Two halves of the fleet on part streams 0 / 1.  Per step and half: ingest, match, then the grid
@@ -891,10 +915,9 @@ int hs_step_ranges_batch_device(hs_ctx *c, int stream_begin, int count, const fl
     if (count == 0) return HS_OK;
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
     int rc = dev_enter(c, s);
-    if (rc == HS_OK) rc = launch_ingest(c, count, d_ranges, range_stride, c->d_ixy, c->max_points, c->d_in, c->d_iorigo, s);
     if (rc == HS_OK)
-        rc = launch_step(c, stream_begin, count, c->d_ixy, c->max_points, c->d_in, c->d_iorigo, d_hints, MODE_PROCESS,
-                         nullptr, nullptr, s);
+        rc = launch_ranges_step(c, stream_begin, count, d_ranges, range_stride, c->d_ixy, c->max_points, c->d_in,
+                                c->d_iorigo, d_hints, nullptr, nullptr, s);
     return rc == HS_OK ? dev_leave(c, s) : rc;
 }
 
@@ -907,11 +930,9 @@ int hs_update_ranges(hs_ctx *c, int stream, const float *ranges, float pose_out[
     if (dev_enter(c, c->stream) != HS_OK) return HS_EHIP;
     if (c->ingest.n > 0)
         HCHK(hipMemcpyAsync(c->d_ranges1, ranges, sizeof(float) * c->ingest.n, hipMemcpyHostToDevice, c->stream));
-    int rc = launch_ingest(c, 1, c->d_ranges1, c->max_points, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, c->stream);
-    if (rc != HS_OK) return rc;
     // scanCallback: startEstimate = getLastScanMatchPose() (hector_slam.cc:201), i.e. no explicit hint
-    rc = launch_step(c, stream, 1, c->d_pts1, c->max_points, c->d_n1, c->d_origo1, nullptr, MODE_PROCESS, c->d_out_pose,
-                     c->d_out_cov, c->stream);
+    int rc = launch_ranges_step(c, stream, 1, c->d_ranges1, c->max_points, c->d_pts1, c->max_points, c->d_n1,
+                                c->d_origo1, nullptr, c->d_out_pose, c->d_out_cov, c->stream);
     if (rc == HS_OK) rc = dev_leave(c, c->stream);
     if (rc != HS_OK) return rc;
     StreamState st;

@@ -101,6 +101,102 @@ __device__ __forceinline__ void solve3(const float *m, const float *b, float *d)
 #undef M
 }
 
+// ---- scan ingest ---------------------------------------------------------------------------------
+// HectorMappingRos::scanCallback (hector_slam.cc:186-198) for a batch of range arrays, one 256-thread
+// workgroup per stream: laser_geometry's projectLaser(scan, cloud, 30.0) (double products of the
+// cached unit vectors, rounded to the float Point32) and rosPointCloudToDataContainer (:320-362)
+// statement by statement, then an order-preserving compaction (wave ballots + a per-chunk prefix over
+// the 4 waves), so point k of the DataContainer is the k-th surviving beam as in the node's loop.
+// hs_ingest_kernel runs it alone; hs_match_kernel runs it as its prologue when handed a MatchIngest
+// (hs_run_ranges_device: one launch less per step, the points go straight into the match registers).
+struct IngestGeom {
+    double cutoff, use_max_sq;
+    double tf[12];  // basis rows, origin
+    float range_min, sqr_min, sqr_max, z_min, z_max, scale;
+    float2 origo;
+    int n;
+};
+
+struct MatchIngest {       // the fused ingest's buffers (ranges == nullptr: points come from xy / counts)
+    const float *ranges;   // [stream][rstride] range arrays
+    int rstride;
+    const double2 *cs;     // unit vectors
+    float2 *xy_out;        // DataContainer points, written for the grid update ([stream][xy_stride])
+    int *n_out;            // point count per stream
+    float2 *origo_out;     // DataContainer origo per stream
+};
+
+// one beam of projectLaser + rosPointCloudToDataContainer: true if it becomes a DataContainer point
+__device__ __forceinline__ bool ingest_beam(const IngestGeom &ig, const double2 *__restrict__ cs, float range, int i,
+                                            float2 &p)
+{
+    bool keep = false;
+    if (((double)range < ig.cutoff) && (range >= ig.range_min)) {  // projectLaser_
+        const double2 u = cs[i];
+        const float x = (float)((double)range * u.x);
+        const float y = (float)((double)range * u.y);
+        const float z = 0.0f;
+        const float d2 = __fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y));          // :334
+        keep = (d2 > ig.sqr_min) && (d2 < ig.sqr_max);                          // :336
+        if ((x < 0.0f) && (d2 < 0.50f)) keep = false;                           // :338-341
+        if ((double)d2 > ig.use_max_sq) keep = false;                           // :344-345
+        if (keep) {
+            const double vx = (double)x, vy = (double)y, vz = (double)z;        // :348 tf dot products
+            const double px = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(ig.tf[0], vx), __dmul_rn(ig.tf[1], vy)),
+                                                  __dmul_rn(ig.tf[2], vz)), ig.tf[9]);
+            const double py = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(ig.tf[3], vx), __dmul_rn(ig.tf[4], vy)),
+                                                  __dmul_rn(ig.tf[5], vz)), ig.tf[10]);
+            const double pz = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(ig.tf[6], vx), __dmul_rn(ig.tf[7], vy)),
+                                                  __dmul_rn(ig.tf[8], vz)), ig.tf[11]);
+            const float zl = (float)(pz - ig.tf[11]);                            // :351
+            keep = zl > ig.z_min && zl < ig.z_max;                               // :353
+            p = make_float2(__fmul_rn((float)px, ig.scale), __fmul_rn((float)py, ig.scale));  // :356
+        }
+    }
+    return keep;
+}
+
+// the whole scan of one stream by a 256-thread workgroup: surviving points in beam order to out (and to
+// stage, an LDS copy, when given); returns the count (uniform).  s_w: 4 ints of LDS.
+__device__ __forceinline__ int ingest_scan(const IngestGeom &ig, const double2 *__restrict__ cs,
+                                           const float *__restrict__ r, float2 *__restrict__ out, float2 *stage,
+                                           int *s_w)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int base = 0;
+    for (int b0 = 0; b0 < ig.n; b0 += 256) {
+        const int i = b0 + tid;
+        float2 p = make_float2(0.0f, 0.0f);
+        const bool keep = i < ig.n && ingest_beam(ig, cs, r[i], i, p);
+        const unsigned long long m = __ballot(keep);
+        if (lane == 0) s_w[wv] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int k = 0; k < wv; ++k) off += s_w[k];
+        if (keep) {
+            const int k = off + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            out[k] = p;
+            if (stage) stage[k] = p;
+        }
+        base += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
+    }
+    return base;
+}
+
+__global__ void __launch_bounds__(256)
+hs_ingest_kernel(IngestGeom ig, const double2 *__restrict__ cs, const float *__restrict__ ranges, int rstride,
+                 float2 *__restrict__ xy, int xy_stride, int *__restrict__ n_out, float2 *__restrict__ origo_out)
+{
+    __shared__ int s_w[4];
+    const int s = blockIdx.x;
+    const int n = ingest_scan(ig, cs, ranges + (size_t)s * rstride, xy + (size_t)s * xy_stride, nullptr, s_w);
+    if (threadIdx.x == 0) {
+        n_out[s] = n;
+        if (origo_out) origo_out[s] = ig.origo;
+    }
+}
+
 // --------------------------------------------------------------------------------- k1: match
 // Per point: OccGridMapUtil::getCompleteHessianDerivs body (H/map/OccGridMapUtil.h:94-126) with
 // interpMapValueWithDerivatives (:139-228), split in two phases so that a thread's gathers for a
@@ -454,7 +550,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
                 const float2 *__restrict__ xy, int xy_stride, const int *__restrict__ counts,
                 const float2 *__restrict__ origo, const float *__restrict__ hints, int stream_begin, int mode,
                 float *__restrict__ out_pose, float *__restrict__ out_cov, PoseLog plog, WorkQueue *__restrict__ wq,
-                UpdList *__restrict__ wl)
+                UpdList *__restrict__ wl, IngestGeom ig, MatchIngest mi)
 {
     static_assert(MATCH_THREADS == 64 * MATCH_WAVES && MATCH_WAVES == 4, "reduction tree assumes 4 waves");
     __shared__ float red[2][MATCH_WAVES][9];
@@ -466,8 +562,15 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     const int s = stream_begin + local;
     StreamState &st = state[s];
     const float *scells = cells + (size_t)s * geom.stream_words;
-    const float2 *pts = xy + (size_t)local * xy_stride;
-    const int n = counts[local];
+    __shared__ int s_w[4];
+    // fused ingest (mi.ranges): the scan's points in beam order to mi.xy_out (for the grid update) and to
+    // an LDS copy in nb_val's space, read into registers below before nb_val's first use
+    float2 *stage = reinterpret_cast<float2 *>(nb_val);
+    const bool fused = mi.ranges != nullptr;
+    const float2 *pts = fused ? mi.xy_out + (size_t)local * xy_stride : xy + (size_t)local * xy_stride;
+    const int n = fused ? ingest_scan(ig, mi.cs, mi.ranges + (size_t)local * mi.rstride,
+                                      mi.xy_out + (size_t)local * xy_stride, stage, s_w)
+                        : counts[local];
 
     float hint[3];
     if (hints) {
@@ -494,8 +597,9 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
 #pragma unroll
         for (int j = 0; j < MATCH_REG_PTS; ++j) {
             const int i = threadIdx.x + j * MATCH_THREADS;
-            preg[j] = (in_regs && i < n) ? pts[i] : make_float2(0.0f, 0.0f);
+            preg[j] = (in_regs && i < n) ? (fused ? stage[i] : pts[i]) : make_float2(0.0f, 0.0f);
         }
+        if (fused) __syncthreads();  // stage read before nb_val is written
         for (int lvl = geom.levels - 1; lvl >= 0; --lvl) {
             const LevelGeom &g = geom.lv[lvl];
             const int iters = lvl == 0 ? 5 : 3;
@@ -556,8 +660,13 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
         st.tot_gn_points += it * (unsigned long long)n;
     }
     st.n = n;
-    st.origo[0] = origo ? origo[local].x : 0.0f;
-    st.origo[1] = origo ? origo[local].y : 0.0f;
+    const float2 org = fused ? ig.origo : (origo ? origo[local] : make_float2(0.0f, 0.0f));
+    st.origo[0] = org.x;
+    st.origo[1] = org.y;
+    if (fused) {
+        mi.n_out[local] = n;
+        mi.origo_out[local] = org;
+    }
     int do_update = 0;
     if (mode == MODE_PROCESS || mode == MODE_NO_MATCH_FORCE) {
         // HectorSlamProcessor::update  H/slam_main/HectorSlamProcessor.h:91-107
@@ -1285,6 +1394,9 @@ constexpr int UPD_FIXED_WORDS = 2 * UPD_MARK_WORDS + 4;  // two mark buffers + f
 
 // the free mark of one raster step: blind LDS atomicMin of the event code
 __device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) { atomicMin(p, ev); }
+#ifndef S2D_WALK
+#define S2D_WALK 2  // 0: sign-mask steps, 2 at a time; 1: borrow-select steps, 2 at a time; 2: as 1, 4 at a time
+#endif
 
 __device__ __forceinline__ int lane_rank(unsigned long long m)  // set lanes below this one
 {
@@ -1487,6 +1599,28 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 int f = da_ - 1 - err;
                 char *pm = reinterpret_cast<char *>(marks) + li * 4;
                 int k = 0;
+#if S2D_WALK == 1 || S2D_WALK == 2
+                // f in [0, da): the minor axis steps when f < db (select form, no sign-mask arithmetic)
+                const int dab2 = dab + dbb;
+#define S2D_WSTEP                                   \
+    do {                                            \
+        upd_mark(reinterpret_cast<unsigned *>(pm), ev); \
+        unsigned fu_;                               \
+        const bool c_ = __builtin_sub_overflow((unsigned)f, (unsigned)db_, &fu_); \
+        f = (int)fu_ + (c_ ? da_ : 0);              \
+        pm += c_ ? dab2 : dab;                      \
+    } while (0)
+#if S2D_WALK == 2
+                for (; k + 3 < scnt; k += 4) {
+                    S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
+                }
+#endif
+                for (; k + 1 < scnt; k += 2) {
+                    S2D_WSTEP; S2D_WSTEP;
+                }
+#undef S2D_WSTEP
+                if (k < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
+#else
                 for (; k + 1 < scnt; k += 2) {
                     upd_mark(reinterpret_cast<unsigned *>(pm), ev);  // bresenhamCellFree (:302-312)
                     int g2 = f - db_;
@@ -1500,6 +1634,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     pm += dab + (m & dbb);
                 }
                 if (k < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
+#endif
             }
             if (__ballot(any) && lane == 0) s_any[buf] = 1u;
         }
@@ -1588,73 +1723,6 @@ __global__ void hs_publish_kernel(const float *__restrict__ lvw, LevelGeom g, in
         const int x = (int)(i % g.sx), y = (int)(i / g.sx);
         const float l = lvw[cell_word(g, x, y)];
         out[i] = l < 0.0f ? (int8_t)0 : (l > 0.0f ? (int8_t)100 : (int8_t)-1);
-    }
-}
-
-// ---- scan ingest ---------------------------------------------------------------------------------
-// HectorMappingRos::scanCallback (hector_slam.cc:186-198) for a batch of range arrays, one 256-thread
-// workgroup per stream: laser_geometry's projectLaser(scan, cloud, 30.0) (double products of the
-// cached unit vectors, rounded to the float Point32) and rosPointCloudToDataContainer (:320-362)
-// statement by statement, then an order-preserving compaction (wave ballots + a per-chunk prefix over
-// the 4 waves), so point k of the DataContainer is the k-th surviving beam as in the node's loop.
-struct IngestGeom {
-    double cutoff, use_max_sq;
-    double tf[12];  // basis rows, origin
-    float range_min, sqr_min, sqr_max, z_min, z_max, scale;
-    float2 origo;
-    int n;
-};
-
-__global__ void __launch_bounds__(256)
-hs_ingest_kernel(IngestGeom ig, const double2 *__restrict__ cs, const float *__restrict__ ranges, int rstride,
-                 float2 *__restrict__ xy, int xy_stride, int *__restrict__ n_out, float2 *__restrict__ origo_out)
-{
-    __shared__ int s_w[4];
-    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const float *r = ranges + (size_t)s * rstride;
-    float2 *out = xy + (size_t)s * xy_stride;
-    int base = 0;
-    for (int b0 = 0; b0 < ig.n; b0 += 256) {
-        const int i = b0 + tid;
-        bool keep = false;
-        float2 p = make_float2(0.0f, 0.0f);
-        if (i < ig.n) {
-            const float range = r[i];
-            if (((double)range < ig.cutoff) && (range >= ig.range_min)) {  // projectLaser_
-                const double2 u = cs[i];
-                const float x = (float)((double)range * u.x);
-                const float y = (float)((double)range * u.y);
-                const float z = 0.0f;
-                const float d2 = __fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y));          // :334
-                keep = (d2 > ig.sqr_min) && (d2 < ig.sqr_max);                          // :336
-                if ((x < 0.0f) && (d2 < 0.50f)) keep = false;                           // :338-341
-                if ((double)d2 > ig.use_max_sq) keep = false;                           // :344-345
-                if (keep) {
-                    const double vx = (double)x, vy = (double)y, vz = (double)z;        // :348 tf dot products
-                    const double px = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(ig.tf[0], vx), __dmul_rn(ig.tf[1], vy)),
-                                                          __dmul_rn(ig.tf[2], vz)), ig.tf[9]);
-                    const double py = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(ig.tf[3], vx), __dmul_rn(ig.tf[4], vy)),
-                                                          __dmul_rn(ig.tf[5], vz)), ig.tf[10]);
-                    const double pz = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(ig.tf[6], vx), __dmul_rn(ig.tf[7], vy)),
-                                                          __dmul_rn(ig.tf[8], vz)), ig.tf[11]);
-                    const float zl = (float)(pz - ig.tf[11]);                            // :351
-                    keep = zl > ig.z_min && zl < ig.z_max;                               // :353
-                    p = make_float2(__fmul_rn((float)px, ig.scale), __fmul_rn((float)py, ig.scale));  // :356
-                }
-            }
-        }
-        const unsigned long long m = __ballot(keep);
-        if (lane == 0) s_w[wv] = __popcll(m);
-        __syncthreads();
-        int off = base;
-        for (int k = 0; k < wv; ++k) off += s_w[k];
-        if (keep) out[off + lane_rank(m)] = p;
-        base += s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        __syncthreads();
-    }
-    if (tid == 0) {
-        n_out[s] = base;
-        if (origo_out) origo_out[s] = ig.origo;
     }
 }
 

@@ -355,10 +355,10 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
             }
             if (i < steps) atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);
         }
-        if (__ballot(any_tile_marks) && (tid & 63) == 0) reinterpret_cast<volatile int *>(s_anyf)[it & 1] = 1;
+        if (__ballot(any_tile_marks) && (tid & 63) == 0) s_anyf[it & 1] = 1;
         gm_lds_barrier();
         // tiles without any mark are not written: their stale stamp makes them read as fresh
-        if (!reinterpret_cast<volatile int *>(s_anyf)[it & 1]) continue;
+        if (!s_anyf[it & 1]) continue;  // plain LDS accesses, ordered by gm_lds_barrier's memory clobber
         any_tile_marks = false;
         unsigned *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
         // acc: the first hitting beam of a cell sums every hit of that cell in beam order (:236-240)

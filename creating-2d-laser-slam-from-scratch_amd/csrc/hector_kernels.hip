@@ -597,7 +597,11 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
 #pragma unroll
         for (int j = 0; j < MATCH_REG_PTS; ++j) {
             const int i = threadIdx.x + j * MATCH_THREADS;
-            preg[j] = (in_regs && i < n) ? (fused ? stage[i] : pts[i]) : make_float2(0.0f, 0.0f);
+            preg[j] = make_float2(0.0f, 0.0f);
+            if (in_regs && i < n) {
+                if (fused) preg[j] = stage[i];  // LDS (kept apart from the global read: no flat access)
+                else preg[j] = pts[i];
+            }
         }
         if (fused) __syncthreads();  // stage read before nb_val is written
         for (int lvl = geom.levels - 1; lvl >= 0; --lvl) {
@@ -1390,7 +1394,7 @@ __device__ __forceinline__ int upd_off(int row, int tiles_x)
 constexpr int UPD_HIT_WORDS = UPD_TH * (TILE / 32);                  // one hit bit per tile cell
 constexpr int UPD_MARK_WORDS = (UPD_TILE_WORDS + UPD_HIT_WORDS + 3) & ~3;
 
-constexpr int UPD_FIXED_WORDS = 2 * UPD_MARK_WORDS + 4;  // two mark buffers + flags; + rays + fan-group boxes
+constexpr int UPD_FIXED_WORDS = 2 * UPD_MARK_WORDS + 4;  // two mark buffers + 4 spare words; then rays, fan-group boxes
 
 // the free mark of one raster step: blind LDS atomicMin of the event code
 __device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) { atomicMin(p, ev); }
@@ -1430,8 +1434,11 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
 {
     extern __shared__ __attribute__((aligned(16))) unsigned smem[];
     // two mark buffers (tile i rasters into buffer i & 1 while tile i - 1's cells are applied),
-    // each UPD_TILE_WORDS event words + UPD_HIT_WORDS hit bits; then 4 flag words, rays, fan boxes
-    volatile unsigned *s_any = smem + 2 * UPD_MARK_WORDS;   // [2] "tile has a mark" per buffer
+    // each UPD_TILE_WORDS event words + UPD_HIT_WORDS hit bits; then 4 spare words, rays, fan boxes
+    // "tile has a mark" per buffer: a plain LDS array (a volatile pointer into smem loses the LDS address
+    // space -- flat accesses with a vmcnt(0) wait that drains the loads the pipeline keeps in flight);
+    // lds_barrier's memory clobber orders the accesses
+    __shared__ unsigned s_any[2];
     unsigned *rays = smem + UPD_FIXED_WORDS;               // max_points packed end cells
     int4 *gbox = reinterpret_cast<int4 *>(rays + ((max_points + 3) & ~3));  // per fan group: x0 y0 x1 y1
     const int lane = threadIdx.x & 63;

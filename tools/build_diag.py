@@ -13,6 +13,8 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   gmplain    WRONG RESULTS  gm_compute_kernel walks with plain LDS stores instead of atomicAdd
   gmnowalk   WRONG RESULTS  gm_compute_kernel clips every line to the tile but skips the walk
   nowalk     WRONG RESULTS  hs_update_kernel clips every ray to the tile but skips the Bresenham walk
+  nosetup    WRONG RESULTS  hs_update_kernel keeps the fan-group culling of every tile, skips every ray
+  noraster   WRONG RESULTS  hs_update_kernel skips the raster loop (tile loop skeleton: clear, barriers)
   visits     same results   hs_update_kernel counts, per (tile, fan group) visit, the lanes with steps,
                             the steps and the wave's longest walk into g_stamps[0..3]
                             (hs_get_queue_stats out[4..7]; tools/diag_update.py prints them)
@@ -40,6 +42,9 @@ PATCHES = {
     "gmnowalk": [("gmapping_kernels.hip", "            int i = 0;\n            for (; i + 1 < steps; i += 2) {",
                   "            int i = steps;\n            for (; i + 1 < steps; i += 2) {")],
     "nowalk": [(K, "                if (scnt <= 0) continue;\n", "                continue;\n")],
+    "nosetup": [(K, "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n",
+                 "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n                continue;\n")],
+    "noraster": [(K, "                const int4 gb = gbox[b0 >> 6];\n", "                if (b0 >= 0) break;\n                const int4 gb = gbox[b0 >> 6];\n")],
     "visits": [(K, "                if (scnt <= 0) continue;\n",
                 "                {\n"
                 "                    const unsigned long long am = __ballot(scnt > 0);\n"

@@ -1650,6 +1650,9 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             // the updateIndex plane is never read --
             // a cell's stored index always predates this scan's marks (currUpdateIndex += 3 per scan)
             int *tu = reinterpret_cast<int *>(pend_tl + TILE_CELLS);
+            // every pending load first (only LDS work came after them): with the loads conditional the
+            // compiler cannot count them and would otherwise wait on each quad's stores before the next
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll
             for (int j = 0; j < UPD_QUADS; ++j) {
                 const unsigned mb = qb[j];

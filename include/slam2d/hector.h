@@ -3,8 +3,8 @@
  * Drop-in boundary: the reference's only polymorphic seam on this path is
  * hectorslam::MapRepresentationInterface (lesson4/include/lesson4/hector_mapping/slam_main/
  * MapRepresentationInterface.h:44-69), owned by HectorSlamProcessor (HectorSlamProcessor.h:61).
- * Each entry point below names the reference member it replaces.  INTEGRATION.md shows the C++
- * adapter `MapRepHip : MapRepresentationInterface` a maintainer would add on the ROS side.
+ * Each entry point below names the reference member it replaces.  include/slam2d/MapRepHip.h is the
+ * C++ adapter `MapRepHip : MapRepresentationInterface` a maintainer adds on the ROS side.
  *
  * Conventions
  *   - plain C types only; poses are float[3] (x, y, theta) in world metres/radians, covariance a
@@ -132,7 +132,9 @@ int hs_set_laser(hs_ctx *ctx, const hs_laser *laser, const double *unit_vectors)
 int hs_ingest_batch_device(hs_ctx *ctx, int count, const float *d_ranges, int range_stride, float *d_xy,
                            int xy_stride, int *d_n, float *d_origo, void *hip_stream);
 /* scanCallback for a batch: ingest every stream's ranges into the context's own point buffers, then
- * one HectorSlamProcessor::update per stream (as hs_step_batch_device; hints NULL = last pose). */
+ * one HectorSlamProcessor::update per stream (as hs_step_batch_device; hints NULL = last pose).  For
+ * scans of <= 1280 beams the ingest runs inside the match kernel (SLAM2D_FUSE_INGEST=0 at hs_create:
+ * a separate kernel); the results are the same bit for bit. */
 int hs_step_ranges_batch_device(hs_ctx *ctx, int stream_begin, int count, const float *d_ranges, int range_stride,
                                 const float *d_hints, void *hip_stream);
 /* scanCallback for `steps` consecutive scans of EVERY stream (offline / bag replay of a whole fleet):

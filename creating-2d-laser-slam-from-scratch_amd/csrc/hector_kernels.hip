@@ -1520,6 +1520,12 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         atomicAdd(&state[s].tot_cells, L);
         atomicAdd(&state[s].tot_rays, R);
     }
+    // both mark buffers start clean (afterwards each tile's readers restore what its raster marked)
+    for (int k = tid; k < 2 * UPD_MARK_WORDS / 4; k += UPD_THREADS)
+        reinterpret_cast<uint4 *>(smem)[k] = (k % (UPD_MARK_WORDS / 4)) < UPD_TILE_WORDS / 4
+                                                 ? make_uint4(W_NONE, W_NONE, W_NONE, W_NONE)
+                                                 : make_uint4(0u, 0u, 0u, 0u);
+    if (tid < 2) s_any[tid] = 0u;
     if (!__syncthreads_or(R != 0)) return;  // no ray drawn on this level
     const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / UPD_TH;
     const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / UPD_TH;
@@ -1530,13 +1536,16 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
 
     const int ntx = tx1 - tx0 + 1, ntiles = ntx * (ty1 - ty0 + 1);
     const int my_tiles = ntiles > part ? (ntiles - part + parts - 1) / parts : 0;
-    // Two-stage pipeline over this workgroup's tiles t_i = part + i * parts:
-    //   iteration i: clear buffer i & 1 -> barrier -> raster tile i -> apply tile i - 1 from registers
-    //   (its cell loads were issued one raster earlier) -> barrier -> read tile i's marks into
-    //   registers and issue the loads of its marked quads.
-    // The barriers only wait for LDS traffic (lds_barrier), so the loads and the previous tile's stores
-    // stay in flight across them.  A buffer is cleared two iterations after its marks were read, with
-    // both barriers of the iteration between.
+    // Two-stage pipeline over this workgroup's tiles t_i = part + i * parts, ONE barrier per tile:
+    //   iteration i: raster tile i into buffer i & 1 -> apply tile i - 1 from registers (its cell loads
+    //   were issued one raster earlier) -> barrier -> read tile i's marks into registers, issue the
+    //   loads of its marked quads and restore the words just read to "no mark".
+    // Every mark word is read and restored by the thread that owns its quad (a hit-bit word by one
+    // lane of the 8 that read it, all in one wave, after the read), so a buffer is clean again before
+    // the barrier of iteration i + 1 that precedes its next raster; a tile without marks wrote
+    // nothing.  s_any[buf] holds the number (i + 1) of the last tile of that buffer that had a mark,
+    // so it needs no reset.  The barrier only waits for LDS traffic (lds_barrier), so the loads and the
+    // previous tile's stores stay in flight across it.
     float4 ql[UPD_QUADS];      // pending tile: log-odds of the marked quads (loads in flight)
     unsigned qb[UPD_QUADS];    // pending tile: 12 mark bits per quad (see apply_cell)
     float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)
@@ -1549,11 +1558,6 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         const int X0 = tx * TILE, Y0 = ty * UPD_TH;
         const int X1 = X0 + TILE, Y1 = Y0 + UPD_TH;
         if (i < my_tiles) {
-            for (int k = tid; k < UPD_MARK_WORDS / 4; k += UPD_THREADS)
-                reinterpret_cast<uint4 *>(marks)[k] = k < UPD_TILE_WORDS / 4 ? make_uint4(W_NONE, W_NONE, W_NONE, W_NONE)
-                                                                            : make_uint4(0u, 0u, 0u, 0u);
-            if (tid == 0) s_any[buf] = 0u;
-            lds_barrier();
             bool any = false;
             for (int b0 = tid & ~63; (b0 & ~255) < n; b0 += UPD_THREADS) {
                 // wave-uniform fan-group test (scalar)
@@ -1643,7 +1647,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 if (k < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
 #endif
             }
-            if (__ballot(any) && lane == 0) s_any[buf] = 1u;
+            if (__ballot(any) && lane == 0) s_any[buf] = (unsigned)(i + 1);
         }
         if (pend_tl) {
             // apply the previous tile: log-odds of every marked cell, both planes written (see below);
@@ -1686,7 +1690,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         }
         if (i < my_tiles) {
             lds_barrier();  // tile i's marks complete
-            if (s_any[buf]) {
+            if (s_any[buf] == (unsigned)(i + 1)) {
                 // thread owns quads q = tid + j * 256 (16 quads per 64-cell row); cells outside the map
                 // (padding of edge tiles) never carry marks
                 pend_tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
@@ -1701,6 +1705,11 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     const unsigned od = (m.x & 1u) | ((m.y & 1u) << 1) | ((m.z & 1u) << 2) | ((m.w & 1u) << 3);
                     qb[j] = mk | ((od & mk) << 4) | ((h & mk) << 8);
                     if (mk) ql[j] = *reinterpret_cast<const float4 *>(&pend_tl[upd_off(row, g.tiles_x) + c4]);
+                    // restore: the quad's event words (read by this thread only) and, by the first of
+                    // the 8 lanes sharing it, the hit-bit word (its readers are this wave's lanes, whose
+                    // read above precedes this write)
+                    if (mk) *reinterpret_cast<uint4 *>(&marks[row * UPD_STRIDE + c4]) = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
+                    if ((tid & 7) == 0) hitb[row * (TILE / 32) + (c4 >> 5)] = 0u;
                 }
             }
         }

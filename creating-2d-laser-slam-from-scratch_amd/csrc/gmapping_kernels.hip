@@ -334,25 +334,29 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
             const int steps = hi - lo + 1;
             nfree += steps;
             any_tile_marks = true;
-            // incremental walk with f = 2 da - 1 - rem: the minor axis steps when f - 2 db < 0; byte
-            // offsets into the count array, branch-free, two steps per trip
+            // incremental walk with f = 2 da - 1 - rem in [0, 2 da): the minor axis steps when f < 2 db --
+            // a subtract with borrow and two selects per step on byte offsets into the count array,
+            // four steps per trip
             const int tda = (int)two_da, tdb = (int)two_db;
-            const int dab = la * 4, dbb = l.sb * lb * 4;
+            const int dab = la * 4, dab2 = dab + l.sb * lb * 4;
             int f = tda - 1 - (int)rem;
             char *pc = reinterpret_cast<char *>(cnt) + li * 4;
             int i = 0;
-            for (; i + 1 < steps; i += 2) {
-                atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);  // visits++ (:227-234)
-                int g2 = f - tdb;
-                int m = g2 >> 31;
-                f = g2 + (m & tda);
-                pc += dab + (m & dbb);
-                atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);
-                g2 = f - tdb;
-                m = g2 >> 31;
-                f = g2 + (m & tda);
-                pc += dab + (m & dbb);
+#define GM_WSTEP                                                                  \
+    do {                                                                          \
+        atomicAdd(reinterpret_cast<unsigned *>(pc), 1u); /* visits++ (:227-234) */ \
+        unsigned fu_;                                                             \
+        const bool c_ = __builtin_sub_overflow((unsigned)f, (unsigned)tdb, &fu_); \
+        f = (int)fu_ + (c_ ? tda : 0);                                            \
+        pc += c_ ? dab2 : dab;                                                    \
+    } while (0)
+            for (; i + 3 < steps; i += 4) {
+                GM_WSTEP; GM_WSTEP; GM_WSTEP; GM_WSTEP;
             }
+            for (; i + 1 < steps; i += 2) {
+                GM_WSTEP; GM_WSTEP;
+            }
+#undef GM_WSTEP
             if (i < steps) atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);
         }
         if (__ballot(any_tile_marks) && (tid & 63) == 0) s_anyf[it & 1] = 1;

@@ -1398,9 +1398,6 @@ constexpr int UPD_FIXED_WORDS = 2 * UPD_MARK_WORDS + 4;  // two mark buffers + 4
 
 // the free mark of one raster step: blind LDS atomicMin of the event code
 __device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) { atomicMin(p, ev); }
-#ifndef S2D_WALK
-#define S2D_WALK 2  // 0: sign-mask steps, 2 at a time; 1: borrow-select steps, 2 at a time; 2: as 1, 4 at a time
-#endif
 
 __device__ __forceinline__ int lane_rank(unsigned long long m)  // set lanes below this one
 {
@@ -1603,49 +1600,31 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 const int ax = w.a0 + w.sa * lo_i - (w.x_major ? X0 : Y0);
                 const int bx = w.b0 + w.sb * q - (w.x_major ? Y0 : X0);
                 const int li = ax * la + bx * lb;
-                // incremental walk, f = da - 1 - error_b: the minor axis steps when f - db < 0; byte
-                // offsets into the mark array, two steps per trip
+                // incremental walk on byte offsets into the mark array, f = da - 1 - error_b
                 const int dab = w.sa * la * 4, dbb = w.sb * lb * 4;
                 const int da_ = w.da, db_ = w.db;
                 int f = da_ - 1 - err;
                 char *pm = reinterpret_cast<char *>(marks) + li * 4;
                 int k = 0;
-#if S2D_WALK == 1 || S2D_WALK == 2
-                // f in [0, da): the minor axis steps when f < db (select form, no sign-mask arithmetic)
+                // f in [0, da): the minor axis steps when f < db -- a subtract with borrow and two selects
+                // per step, four steps per trip
                 const int dab2 = dab + dbb;
-#define S2D_WSTEP                                   \
-    do {                                            \
-        upd_mark(reinterpret_cast<unsigned *>(pm), ev); \
-        unsigned fu_;                               \
+#define S2D_WSTEP                                                                 \
+    do {                                                                          \
+        upd_mark(reinterpret_cast<unsigned *>(pm), ev); /* bresenhamCellFree */   \
+        unsigned fu_;                                                             \
         const bool c_ = __builtin_sub_overflow((unsigned)f, (unsigned)db_, &fu_); \
-        f = (int)fu_ + (c_ ? da_ : 0);              \
-        pm += c_ ? dab2 : dab;                      \
+        f = (int)fu_ + (c_ ? da_ : 0);                                            \
+        pm += c_ ? dab2 : dab;                                                    \
     } while (0)
-#if S2D_WALK == 2
                 for (; k + 3 < scnt; k += 4) {
                     S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
                 }
-#endif
                 for (; k + 1 < scnt; k += 2) {
                     S2D_WSTEP; S2D_WSTEP;
                 }
 #undef S2D_WSTEP
                 if (k < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
-#else
-                for (; k + 1 < scnt; k += 2) {
-                    upd_mark(reinterpret_cast<unsigned *>(pm), ev);  // bresenhamCellFree (:302-312)
-                    int g2 = f - db_;
-                    int m = g2 >> 31;
-                    f = g2 + (m & da_);
-                    pm += dab + (m & dbb);
-                    upd_mark(reinterpret_cast<unsigned *>(pm), ev);
-                    g2 = f - db_;
-                    m = g2 >> 31;
-                    f = g2 + (m & da_);
-                    pm += dab + (m & dbb);
-                }
-                if (k < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
-#endif
             }
             if (__ballot(any) && lane == 0) s_any[buf] = (unsigned)(i + 1);
         }

@@ -37,12 +37,9 @@ PATCHES = {
                "{ *reinterpret_cast<volatile unsigned *>(p) = ev; }")],
     "noapply": [(K, "        if (pend_tl) {\n", "        if (pend_tl && false) {\n")],
     "hwexp": [(K, "    float odds = sdm_expf(l);", "    float odds = __expf(l);")],
-    "gmplain": [("gmapping_kernels.hip", "            for (; i + 1 < steps; i += 2) {\n                atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);",
-                 "            for (; i + 1 < steps; i += 2) {\n                *reinterpret_cast<volatile unsigned *>(pc) = 1u;"),
-                ("gmapping_kernels.hip", "                pc += dab + (m & dbb);\n                atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);",
-                 "                pc += dab + (m & dbb);\n                *reinterpret_cast<volatile unsigned *>(pc) = 1u;")],
-    "gmnowalk": [("gmapping_kernels.hip", "            int i = 0;\n            for (; i + 1 < steps; i += 2) {",
-                  "            int i = steps;\n            for (; i + 1 < steps; i += 2) {")],
+    "gmplain": [("gmapping_kernels.hip", "        atomicAdd(reinterpret_cast<unsigned *>(pc), 1u); /* visits++ (:227-234) */ \\\n",
+                 "        *reinterpret_cast<volatile unsigned *>(pc) = 1u;                             \\\n")],
+    "gmnowalk": [("gmapping_kernels.hip", "            int i = 0;\n#define GM_WSTEP", "            int i = steps;\n#define GM_WSTEP")],
     "nowalk": [(K, "                if (scnt <= 0) continue;\n", "                continue;\n")],
     "nosetup": [(K, "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n",
                  "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n                continue;\n")],

@@ -69,10 +69,19 @@ __device__ __forceinline__ bool pose_diff_larger(const float *p1, const float *p
     return fabsf(ad) > ang;
 }
 
+// exp's 2^(j/128) table (detmath.h): read once per workgroup into LDS by the kernels that call
+// cell_prob (hs_match_kernel, load_exptab), so the per-lane table reads are LDS reads
+__constant__ double c_exptab[SDM_EXPTAB_N] = {SDM_EXPTAB_VALUES};
+__shared__ double s_exptab[SDM_EXPTAB_N];
+__device__ __forceinline__ void load_exptab()  // all threads; a barrier must follow before cell_prob
+{
+    for (int k = threadIdx.x; k < SDM_EXPTAB_N; k += blockDim.x) s_exptab[k] = c_exptab[k];
+}
+
 // GridMapLogOddsFunctions::getGridProbability  H/map/GridMapLogOdds.h:136-140
 __device__ __forceinline__ float cell_prob(float l)
 {
-    float odds = sdm_expf(l);
+    float odds = sdm_expf_tab(l, s_exptab);
     return __fdiv_rn(odds, odds + 1.0f);
 }
 
@@ -561,6 +570,8 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     const int local = blockIdx.x;
     const int s = stream_begin + local;
     StreamState &st = state[s];
+    load_exptab();
+    __syncthreads();
     const float *scells = cells + (size_t)s * geom.stream_words;
     __shared__ int s_w[4];
     // fused ingest (mi.ranges): the scan's points in beam order to mi.xy_out (for the grid update) and to

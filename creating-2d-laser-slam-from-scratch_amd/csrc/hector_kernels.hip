@@ -1575,51 +1575,42 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
                 const int b = fan_beam(b0, lane);
                 const unsigned r = b < n ? rays[b] : RAY_INVALID;
-                int scnt = 0;           // free steps of this beam inside the tile
-                RayWalk w = {};
-                int lo_i = 0, q = 0, err = 0;
-                if (r != RAY_INVALID) {
-                    const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-                    if (!(max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1)) {
-                        if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {  // bresenhamCellOcc (:266)
-                            const int c = (y1 - Y0) * TILE + (x1 - X0);
-                            atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
-                            atomicOr(&hitb[c >> 5], 1u << (c & 31));
-                            any = true;
-                        }
-                        w = ray_walk(x0, y0, x1, y1);
-                        int hi_i;
-                        const bool in = w.x_major ? walk_range(w, X0, X1, Y0, Y1, lo_i, hi_i)
-                                                  : walk_range(w, Y0, Y1, X0, X1, lo_i, hi_i);
-                        if (in) {
-                            if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
-                            if (lo_i <= hi_i) {
-                                scnt = hi_i - lo_i + 1;
-                                const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
-                                q = (int)udiv_small(num, (unsigned)w.da);
-                                err = (int)(num - (unsigned)q * (unsigned)w.da);
-                                any = true;
-                            }
-                        }
-                    }
+                if (r == RAY_INVALID) continue;
+                const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+                if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
+                if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {  // bresenhamCellOcc (:266)
+                    const int c = (y1 - Y0) * TILE + (x1 - X0);
+                    atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
+                    atomicOr(&hitb[c >> 5], 1u << (c & 31));
+                    any = true;
                 }
-                if (scnt <= 0) continue;
+                const RayWalk w = ray_walk(x0, y0, x1, y1);
+                // the tile in (major, minor) order, selected before ONE clip (lanes of a fan that straddles
+                // a diagonal differ in x_major)
+                const int A0 = w.x_major ? X0 : Y0, A1 = w.x_major ? X1 : Y1;
+                const int B0 = w.x_major ? Y0 : X0, B1 = w.x_major ? Y1 : X1;
+                int lo_i, hi_i;
+                if (!walk_range(w, A0, A1, B0, B1, lo_i, hi_i)) continue;
+                if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
+                if (lo_i > hi_i) continue;
+                any = true;
+                const int scnt = hi_i - lo_i + 1;     // free steps of this beam inside the tile
+                const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
+                const int q = (int)udiv_small(num, (unsigned)w.da);
+                const int err = (int)(num - (unsigned)q * (unsigned)w.da);
                 const unsigned ev = 2u * (unsigned)b + 1u;
                 // LDS index of step lo_i and its increments along the major / minor axis
                 const int la = w.x_major ? 1 : UPD_STRIDE;
                 const int lb = w.x_major ? UPD_STRIDE : 1;
-                const int ax = w.a0 + w.sa * lo_i - (w.x_major ? X0 : Y0);
-                const int bx = w.b0 + w.sb * q - (w.x_major ? Y0 : X0);
-                const int li = ax * la + bx * lb;
-                // incremental walk on byte offsets into the mark array, f = da - 1 - error_b
-                const int dab = w.sa * la * 4, dbb = w.sb * lb * 4;
+                const int li = (w.a0 + w.sa * lo_i - A0) * la + (w.b0 + w.sb * q - B0) * lb;
+                // incremental walk on byte offsets into the mark array, f = da - 1 - error_b in [0, da):
+                // the minor axis steps when f < db -- a subtract with borrow and two selects per step,
+                // four steps per trip
+                const int dab = w.sa * la * 4, dab2 = dab + w.sb * lb * 4;
                 const int da_ = w.da, db_ = w.db;
                 int f = da_ - 1 - err;
                 char *pm = reinterpret_cast<char *>(marks) + li * 4;
                 int k = 0;
-                // f in [0, da): the minor axis steps when f < db -- a subtract with borrow and two selects
-                // per step, four steps per trip
-                const int dab2 = dab + dbb;
 #define S2D_WSTEP                                                                 \
     do {                                                                          \
         upd_mark(reinterpret_cast<unsigned *>(pm), ev); /* bresenhamCellFree */   \

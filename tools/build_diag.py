@@ -15,11 +15,6 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   nowalk     WRONG RESULTS  hs_update_kernel clips every ray to the tile but skips the Bresenham walk
   nosetup    WRONG RESULTS  hs_update_kernel keeps the fan-group culling of every tile, skips every ray
   noraster   WRONG RESULTS  hs_update_kernel skips the raster loop (tile loop skeleton: clear, barriers)
-  visits2    same results   as visits: visits, visits with no walking lane, walking lanes, lanes that
-                            passed the ray-vs-tile box test (set up a walk)
-  visits     same results   hs_update_kernel counts, per (tile, fan group) visit, the lanes with steps,
-                            the steps and the wave's longest walk into g_stamps[0..3]
-                            (hs_get_queue_stats out[4..7]; tools/diag_update.py prints them)
 """
 import os
 import shutil
@@ -36,45 +31,15 @@ PATCHES = {
                "__device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) "
                "{ *reinterpret_cast<volatile unsigned *>(p) = ev; }")],
     "noapply": [(K, "        if (pend_tl) {\n", "        if (pend_tl && false) {\n")],
-    "hwexp": [(K, "    float odds = sdm_expf(l);", "    float odds = __expf(l);")],
+    "hwexp": [(K, "    float odds = sdm_expf_tab(l, s_exptab);", "    float odds = __expf(l);")],
     "gmplain": [("gmapping_kernels.hip", "        atomicAdd(reinterpret_cast<unsigned *>(pc), 1u); /* visits++ (:227-234) */ \\\n",
                  "        *reinterpret_cast<volatile unsigned *>(pc) = 1u;                             \\\n")],
     "gmnowalk": [("gmapping_kernels.hip", "            int i = 0;\n#define GM_WSTEP", "            int i = steps;\n#define GM_WSTEP")],
-    "nowalk": [(K, "                if (scnt <= 0) continue;\n", "                continue;\n")],
+    "nowalk": [(K, "                if (lo_i > hi_i) continue;\n                any = true;\n",
+                "                if (lo_i > hi_i) continue;\n                any = true;\n                continue;\n")],
     "nosetup": [(K, "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n",
                  "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n                continue;\n")],
     "noraster": [(K, "                const int4 gb = gbox[b0 >> 6];\n", "                if (b0 >= 0) break;\n                const int4 gb = gbox[b0 >> 6];\n")],
-    "visits2": [(K, "                int scnt = 0;           // free steps of this beam inside the tile\n",
-                 "                int scnt = 0;           // free steps of this beam inside the tile\n                bool dsu = false;\n"),
-                (K, "                        w = ray_walk(x0, y0, x1, y1);\n",
-                 "                        dsu = true;\n                        w = ray_walk(x0, y0, x1, y1);\n"),
-                (K, "                if (scnt <= 0) continue;\n",
-                 "                {\n"
-                 "                    const unsigned long long am = __ballot(scnt > 0), ad = __ballot(dsu);\n"
-                 "                    if (lane == 0) {\n"
-                 "                        atomicAdd(&g_stamps[0], 1ull);\n"
-                 "                        atomicAdd(&g_stamps[1], am ? 0ull : 1ull);\n"
-                 "                        atomicAdd(&g_stamps[2], (unsigned long long)__popcll(am));\n"
-                 "                        atomicAdd(&g_stamps[3], (unsigned long long)__popcll(ad));\n"
-                 "                    }\n"
-                 "                }\n"
-                 "                if (scnt <= 0) continue;\n")],
-    "visits": [(K, "                if (scnt <= 0) continue;\n",
-                "                {\n"
-                "                    const unsigned long long am = __ballot(scnt > 0);\n"
-                "                    int mx = scnt, sm = scnt;\n"
-                "                    for (int off = 32; off >= 1; off >>= 1) {\n"
-                "                        mx = max(mx, __shfl_xor(mx, off, 64));\n"
-                "                        sm += __shfl_xor(sm, off, 64);\n"
-                "                    }\n"
-                "                    if (lane == 0) {\n"
-                "                        atomicAdd(&g_stamps[0], 1ull);\n"
-                "                        atomicAdd(&g_stamps[1], (unsigned long long)__popcll(am));\n"
-                "                        atomicAdd(&g_stamps[2], (unsigned long long)sm);\n"
-                "                        atomicAdd(&g_stamps[3], (unsigned long long)mx);\n"
-                "                    }\n"
-                "                }\n"
-                "                if (scnt <= 0) continue;\n")],
 }
 
 

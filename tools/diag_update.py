@@ -23,11 +23,3 @@ q = f.queue_stats(); kt = f.kernel_times()
 print("kernel ms:", kt)
 tot = q["cyc_setup"] + q["cyc_raster"] + q["cyc_apply"]
 blocks = B * (1 if os.environ.get("LVL_ONLY") else 3)
-if os.environ.get("VISITS2"):  # SLAM2D_LIB=.../libslam2d_visits2.so
-    v, e, a, d = q["cyc_setup"], q["cyc_raster"], q["cyc_apply"], q["tiles"]
-    print("visits %d per scan %.1f; empty visits %.3f; walking lanes/visit %.1f; set-up lanes/visit %.1f"
-          % (v, v / B, e / v, a / v, d / v))
-if os.environ.get("VISITS"):  # SLAM2D_LIB=.../libslam2d_visits.so (tools/build_diag.py visits)
-    v, a, st, mx = q["cyc_setup"], q["cyc_raster"], q["cyc_apply"], q["tiles"]
-    print("(tile, fan group) visits %d per scan %.1f; active lanes/visit %.1f, steps/visit %.1f, longest walk/visit "
-          "%.1f, walk lane utilisation %.3f" % (v, v / B, a / v, st / v, mx / v, st / (64.0 * mx)))

@@ -243,7 +243,7 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         int blocks = 0;
         for (int U = 1; U <= count; ++U) {
             int pl[MAX_LEVELS], b = 0;
-            upd_split(U, c->ncu, c->levels, pl);
+            upd_split(U, c->ncu, c->levels, pl, c->geom.upd_minp);
             for (int l = 0; l < c->levels; ++l) b += pl[l] * U;
             blocks = b > blocks ? b : blocks;
         }
@@ -480,6 +480,17 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
                 if (*q == ',') ++q;
             }
             for (; l < MAX_LEVELS; ++l) c->geom.upd_parts[l] = c->geom.upd_parts[l - 1];
+        }
+        // list-driven split: minimum workgroups per level, SLAM2D_UPD_SPLIT="m0,m1,..." (default: upd_split's)
+        for (int l = 0; l < MAX_LEVELS; ++l) c->geom.upd_minp[l] = 0;
+        if (const char *us = getenv("SLAM2D_UPD_SPLIT")) {
+            int l = 0;
+            for (const char *q = us; *q && l < MAX_LEVELS; ++l) {
+                const int v = atoi(q);
+                c->geom.upd_minp[l] = v < 0 ? 0 : (v > 64 ? 64 : v);
+                while (*q && *q != ',') ++q;
+                if (*q == ',') ++q;
+            }
         }
         if (c->nparts < 1) c->nparts = 1;
         if (c->nparts > MAX_PARTS) c->nparts = MAX_PARTS;

@@ -59,6 +59,7 @@ struct FleetGeom {
     float min_dist, min_ang;   // map update thresholds
     size_t stream_words;       // 4-byte words per stream (all levels, tiled, both planes)
     int upd_parts[MAX_LEVELS]; // hs_update_kernel workgroups per (stream, level)
+    int upd_minp[MAX_LEVELS];  // list-driven split: at least this many workgroups per level (0: upd_split's)
     LevelGeom lv[MAX_LEVELS];
 };
 
@@ -115,13 +116,14 @@ struct UpdList {
 // Workgroups per (stream, level) of hs_update_kernel for U updating streams on ncu CUs: about 4 level-0
 // workgroups per CU for small batches (2 for U <= 32), at least 2 for level 0, halved per level
 // (measured).
-inline __host__ __device__ void upd_split(int U, int ncu, int levels, int *parts)
+inline __host__ __device__ void upd_split(int U, int ncu, int levels, int *parts, const int *minp)
 {
     const int target = U <= 32 ? 2 : 4;
     int p0 = U > 0 ? (target * ncu + U - 1) / U : 1;
     if (p0 < 2) p0 = 2;
     for (int l = 0; l < levels; ++l) {
-        const int v = p0 >> l;
+        int v = p0 >> l;
+        if (v < minp[l]) v = minp[l];
         parts[l] = v < 1 ? 1 : (v > 64 ? 64 : v);
     }
 }

@@ -1460,7 +1460,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         const int U = wl->count;
         if (blockIdx.x == 0 && threadIdx.x == 0) wl_next->count = 0;
         int pl[MAX_LEVELS];
-        upd_split(U, ncu, geom.levels, pl);
+        upd_split(U, ncu, geom.levels, pl, geom.upd_minp);
         while (lvl + 1 < geom.levels && idx >= pl[lvl] * U) idx -= pl[lvl++] * U;
         if (idx >= pl[lvl] * U) return;  // the grid is sized for the largest split (host)
         parts = pl[lvl];

@@ -175,6 +175,67 @@ def _maps_equal(fa, fb, S, LV):
             assert np.array_equal(_bits(ma["logodds"]), _bits(mb["logodds"])), (s, lvl)
 
 
+@pytest.mark.parametrize("S,gate", [(5, (-1.0, -1.0)), (4, (0.4, 0.9))])
+def test_fused_ingest_equals_separate_kernel(gpu, monkeypatch, S, gate):
+    """Range-array steps run the scan ingest inside hs_match_kernel (default) or as hs_ingest_kernel
+    (SLAM2D_FUSE_INGEST=0 at hs_create): every pose, gate and map cell equal bit for bit."""
+    import torch
+    T, LV, SIZE = 6, 2, 384
+    scans = synth.make_streams(S, T, with_points=False, seed=91)
+    L = _roll_pi_laser()
+    monkeypatch.setenv("SLAM2D_FUSE_INGEST", "0")
+    fa = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
+    monkeypatch.delenv("SLAM2D_FUSE_INGEST")
+    fb = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
+    for f in (fa, fb):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(*gate)
+        f.set_laser(L)
+    r = np.ascontiguousarray(scans.ranges.transpose(1, 0, 2))      # [T][S][N]
+    d_r = torch.from_numpy(r).cuda()
+    hs = torch.cuda.current_stream().cuda_stream
+    for t in range(T):
+        fa.step_ranges_device(d_r[t].data_ptr(), N, hip_stream=hs)
+        fb.step_ranges_device(d_r[t].data_ptr(), N, hip_stream=hs)
+    torch.cuda.synchronize()
+    pa, ca, da, _ = fa.poses()
+    pb, cb, db, _ = fb.poses()
+    assert np.array_equal(_bits(pa), _bits(pb)) and np.array_equal(_bits(ca), _bits(cb))
+    assert np.array_equal(da, db)
+    _maps_equal(fa, fb, S, LV)
+    fa.close()
+    fb.close()
+
+
+def test_update_split_knob_same_maps(gpu, monkeypatch):
+    """SLAM2D_UPD_SPLIT (more grid-update workgroups per level) changes only the work split: maps and
+    poses equal the default split bit for bit."""
+    import torch
+    S, T, LV, SIZE = 3, 5, 3, 512
+    scans = synth.make_streams(S, T, with_points=False, seed=17)
+    L = _roll_pi_laser()
+    monkeypatch.setenv("SLAM2D_UPD_SPLIT", "5,3,2")
+    fa = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
+    monkeypatch.delenv("SLAM2D_UPD_SPLIT")
+    fb = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
+    for f in (fa, fb):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(-1.0, -1.0)
+        f.set_laser(L)
+    r = np.ascontiguousarray(scans.ranges.transpose(1, 0, 2))
+    d_r = torch.from_numpy(r).cuda()
+    hs = torch.cuda.current_stream().cuda_stream
+    for f in (fa, fb):
+        f.run_ranges_device(T, d_r.data_ptr(), N, S * N, hip_stream=hs)
+    torch.cuda.synchronize()
+    pa, _, _, _ = fa.poses()
+    pb, _, _, _ = fb.poses()
+    assert np.array_equal(_bits(pa), _bits(pb))
+    _maps_equal(fa, fb, S, LV)
+    fa.close()
+    fb.close()
+
+
 @pytest.mark.parametrize("S,gate,pipeline", [(7, (-1.0, -1.0), "1"), (6, (0.4, 0.9), "1"), (1, (-1.0, -1.0), "1"),
                                              (5, (0.4, 0.9), "0")])
 def test_run_ranges_equals_per_step(gpu, monkeypatch, S, gate, pipeline):

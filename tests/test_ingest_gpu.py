@@ -149,6 +149,45 @@ def test_step_ranges_matches_oracle_pipeline(gpu):
             assert np.array_equal(_bits(m["logodds"]), _bits(ol))
 
 
+def test_step_ranges_wide_scan_separate_ingest(gpu):
+    """Scans of more than 1280 beams do not fit the match kernel's registers: the ingest runs as its own
+    kernel and the match takes its strided path -- still equal to oracle.ingest -> oracle process."""
+    import torch
+    NB = 1440
+    S, T, LV, SIZE = 2, 6, 2, 512
+    scans = synth.make_streams(S, T, with_points=False, seed=3, n_beams=NB)
+    ang = synth.beam_angles(NB)
+    L = HsLaser.defaults(NB, float(ang[0]), float(ang[1] - ang[0]))
+    cs = np.ascontiguousarray(np.stack([np.cos(ang), np.sin(ang)], 1))
+    fleet = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=NB)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(-1.0, -1.0)
+    fleet.set_laser(L, unit_vectors=cs)
+    oras = [O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=256) for _ in range(S)]
+    for o in oras:
+        o.set_update_factors(0.4, 0.9)
+        o.set_thresholds(-1.0, -1.0)
+    scale = fleet.scale_to_map()
+    for t in range(T):
+        r = np.ascontiguousarray(scans.ranges[:, t, :])
+        d_r = torch.from_numpy(r).cuda()
+        fleet.step_ranges_device(d_r.data_ptr(), NB)
+        gp, _, gd, _ = fleet.poses()
+        for s in range(S):
+            pts, org = O.ingest(r[s], cs, L.as_oracle_dict(), scale)
+            assert pts.shape[0] > 1280  # the wide path
+            op, _, od = oras[s].process(pts, origo=tuple(org))
+            assert gd[s] == od, (t, s)
+            assert np.array_equal(_bits(gp[s]), _bits(op)), (t, s, gp[s], op)
+    for s in range(S):
+        for lvl in range(LV):
+            m = fleet.get_map(s, lvl)
+            ol, ou = oras[s].level(lvl)
+            assert np.array_equal(m["upd"], ou)
+            assert np.array_equal(_bits(m["logodds"]), _bits(ol))
+    fleet.close()
+
+
 def test_update_ranges_host_entry_equals_batch(gpu):
     import torch
     scans = synth.make_streams(1, 6, with_points=False)

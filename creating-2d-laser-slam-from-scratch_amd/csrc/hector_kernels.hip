@@ -784,6 +784,17 @@ __device__ __forceinline__ unsigned make_ray(const LevelGeom &g, const RayFrame 
 // correction step each way -- ~8 instructions instead of the ~25 of the integer division sequence.
 // Exact whenever the quotient is < 2^16, which covers every step index (<= 32767) it is compared
 // with; a larger quotient stays > 2^15 and only ever means "beyond the walk".
+__device__ __forceinline__ unsigned udiv_rcp(unsigned n, unsigned d, float rcp_d)  // rcp_d = rcp((float)d)
+{
+    unsigned q = (unsigned)((float)n * rcp_d);
+    int r = (int)(n - q * d);
+    if (r < 0) {
+        --q;
+        r += (int)d;
+    }
+    if (r >= (int)d) ++q;
+    return q;
+}
 __device__ __forceinline__ unsigned udiv_small(unsigned n, unsigned d)
 {
 #if S2D_FAST_UDIV
@@ -825,38 +836,29 @@ __device__ __forceinline__ RayWalk ray_walk(int x0, int y0, int x1, int y1)
 // returns false if none.  q(i) >= Q  <=>  i >= ceil((Q*da - e0)/db);  q(i) <= Q  <=>  i <= floor(((Q+1)*da - e0 - 1)/db).
 __device__ __forceinline__ bool walk_range(const RayWalk &w, int A0, int A1, int B0, int B1, int &lo, int &hi)
 {
-    int ilo, ihi;
-    if (w.sa > 0) {
-        ilo = A0 - w.a0;
-        ihi = A1 - 1 - w.a0;
-    } else {
-        ilo = w.a0 - (A1 - 1);
-        ihi = w.a0 - A0;
+    // branch-free (lanes of one fan differ in the step signs): the steps whose major coordinate lies in
+    // [A0, A1), then the minor constraint q(i) in [qlo, qhi] through the two divisions by db (one
+    // reciprocal), each taken only where its numerator is meaningful (qlo > 0 / qhi >= 0, db > 0)
+    const int d0 = A0 - w.a0, d1 = A1 - 1 - w.a0;
+    lo = w.sa > 0 ? d0 : -d1;
+    hi = w.sa > 0 ? d1 : -d0;
+    lo = lo > 0 ? lo : 0;
+    hi = hi < w.da ? hi : w.da;
+    const int e0 = B0 - w.b0, e1 = B1 - 1 - w.b0;
+    const int qlo = w.sb > 0 ? e0 : -e1, qhi = w.sb > 0 ? e1 : -e0;
+    const unsigned dbs = w.db ? (unsigned)w.db : 1u;
+    const float rdb = __builtin_amdgcn_rcpf((float)dbs);
+    // numerator > 0 when qlo > 0: qlo * da - e0 >= da - da / 2
+    const int n1 = qlo > 0 ? qlo * w.da - w.e0 + w.db - 1 : 0;
+    // numerator >= 0 when qhi >= 0: (qhi + 1) * da - e0 - 1 >= da - da / 2 - 1
+    const int n2 = qhi >= 0 ? (qhi + 1) * w.da - w.e0 - 1 : 0;
+    const int t = (int)udiv_rcp((unsigned)n1, dbs, rdb), t2 = (int)udiv_rcp((unsigned)n2, dbs, rdb);
+    if (w.db != 0) {
+        if (qlo > 0 && t > lo) lo = t;
+        if (t2 < hi) hi = t2;
     }
-    lo = ilo > 0 ? ilo : 0;
-    hi = ihi < w.da ? ihi : w.da;
-    if (lo > hi) return false;
-    int qlo, qhi;
-    if (w.sb > 0) {
-        qlo = B0 - w.b0;
-        qhi = B1 - 1 - w.b0;
-    } else {
-        qlo = w.b0 - (B1 - 1);
-        qhi = w.b0 - B0;
-    }
-    if (qhi < 0) return false;
-    if (w.db == 0) {
-        if (qlo > 0) return false;  // q(i) == 0 for every step
-        return true;
-    }
-    if (qlo > 0) {  // numerator > 0: qlo * da - e0 >= da - da / 2
-        int t = (int)udiv_small((unsigned)(qlo * w.da - w.e0 + w.db - 1), (unsigned)w.db);
-        if (t > lo) lo = t;
-    }
-    // numerator >= 0: (qhi + 1) * da - e0 - 1 >= da - da / 2 - 1
-    int t2 = (int)udiv_small((unsigned)((qhi + 1) * w.da - w.e0 - 1), (unsigned)w.db);
-    if (t2 < hi) hi = t2;
-    return lo <= hi;
+    // db == 0: q(i) == 0 for every step, so the walk is in the band iff qlo <= 0 <= qhi
+    return lo <= hi && qhi >= 0 && !(w.db == 0 && qlo > 0);
 }
 
 // ------------------------------------------------------------ k2/k3: binned, tiled grid update

@@ -19,7 +19,7 @@ import csv, glob, sys, collections
 agg = collections.defaultdict(float); cnt = collections.Counter()
 for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("s2d::", "")
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("s2d::", "")
         agg[(k, r["Counter_Name"])] += float(r["Counter_Value"]); cnt[(k, r["Counter_Name"])] += 1
 for (k, c), v in sorted(agg.items()):
     if k.startswith(("hs_", "kt_", "gm_", "pl_")): print(f"{k:24s} {c:24s} {v/ max(cnt[(k,c)],1):18.0f} (per dispatch avg over {cnt[(k,c)]})")

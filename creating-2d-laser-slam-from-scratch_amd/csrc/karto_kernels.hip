@@ -700,29 +700,26 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
                         tile[((r + KT_AS_MARGIN) * KT_AS_TW + KT_AS_MARGIN) / 8 + (q & 7)] = gw[(size_t)y * wsw + xq];
                 }
             if (ks <= KT_FAST_KS) {
-                // lanes that own no kernel cell in slot u work on a private trash byte, so no two lanes
-                // of one store ever address the same byte
-                int coff[4];
-                bool own[4];
+                // A lane that owns no kernel cell in slot u (its kernel value is 0, so it writes back what it
+                // read) addresses byte (ks rows below the footprint's origin) + lane: outside the footprint's
+                // rows, so never a byte an owning lane of the same store writes, and inside the tile
+                // buffer (origin row <= 16 + 63, + 15 rows, + 142 bytes < 96 * 96 + 64).  Every address is
+                // then the scalar item origin plus a per-lane constant: one add per slot.
+                unsigned char *tb[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    own[u] = lane + 64 * u < ks * ks;
-                    coff[u] = cell_dy[u] * KT_AS_TW + cell_dx[u];
+                    const bool own = lane + 64 * u < ks * ks;
+                    tb[u] = tileb + (own ? cell_dy[u] * KT_AS_TW + cell_dx[u] : ks * KT_AS_TW + lane);
                 }
-                const int trash = KT_AS_TW * KT_AS_TW + lane;
-                const int base = (KT_AS_MARGIN - h - y0) * KT_AS_TW + (KT_AS_MARGIN - h - x0);
+                const int base = __builtin_amdgcn_readfirstlane((KT_AS_MARGIN - h - y0) * KT_AS_TW + (KT_AS_MARGIN - h - x0));
                 for (int c = c0; c < c1; ++c) {
-                    const unsigned cell = sitem[c];
-                    const int o = base + (int)(cell >> 16) * KT_AS_TW + (int)(cell & 0xFFFFu);
-                    int ad[4];
+                    const unsigned cell = (unsigned)__builtin_amdgcn_readfirstlane((int)sitem[c]);
+                    const int o = base + (int)(cell >> 16) * KT_AS_TW + (int)(cell & 0xFFFFu);  // scalar
                     unsigned cur[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        ad[u] = own[u] ? o + coff[u] : trash;
-                        cur[u] = tileb[ad[u]];
-                    }
+                    for (int u = 0; u < 4; ++u) cur[u] = tb[u][o];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) tileb[ad[u]] = (unsigned char)max(cur[u], (unsigned)cell_kv[u]);
+                    for (int u = 0; u < 4; ++u) tb[u][o] = (unsigned char)max(cur[u], (unsigned)cell_kv[u]);
                 }
             } else {
                 for (int c = c0; c < c1; ++c) {

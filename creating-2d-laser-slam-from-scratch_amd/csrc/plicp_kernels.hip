@@ -58,18 +58,106 @@ __device__ __forceinline__ double pl_dist_to_segment(double ax, double ay, doubl
     return sqrt((qx - x) * (qx - x) + (qy - y) * (qy - y));
 }
 
-// possible_interval (CSM icp_corr_dumb.c)
+// Every atan / atan2 on the correspondence path only feeds an integer (a cell index or a window
+// half-width) through a monotone double expression.  So each is first evaluated by a cheap float
+// approximation a with |a - exact| < PL_ATAN_EPS (measured by tools/check_fatan.c: 2.3e-7 worst case
+// over every non-negative float for pl_fatan, 4.1e-7 over 2e8 sampled double pairs for pl_fatan2, the
+// double -> float rounding of the arguments included; NaN / inf fall to the exact path): the integer the expression yields at a - eps and at a + eps brackets
+// the exact one, and when the two agree that is the result -- the exact double evaluation (the
+// reference's value, sdm_atan / sdm_atan2) runs only when the bracket straddles an integer boundary
+// (about 2 eps / cell width, < 1e-3 of the evaluations).  Results are the exact path's, bit for bit.
+constexpr double PL_ATAN_EPS = 2e-6;
+
+// atan(t), t in [0, 1]: t * P(t^2), degree-7 least-squares fit on Chebyshev nodes, float Horner
+__device__ __forceinline__ float pl_fatan01(float t)
+{
+    const float z = t * t;
+    float q = -0.003962602f;
+    q = 0.021518489f + z * q;
+    q = -0.055396412f + z * q;
+    q = 0.096028686f + z * q;
+    q = -0.13892588f + z * q;
+    q = 0.19943212f + z * q;
+    q = -0.33329552f + z * q;
+    q = 0.99999923f + z * q;
+    return t * q;
+}
+// atan(x), x >= 0
+__device__ __forceinline__ float pl_fatan(float x)
+{
+    return x > 1.0f ? 1.5707963f - pl_fatan01(1.0f / x) : pl_fatan01(x);
+}
+// atan2(y, x) for x, y != 0 (the caller takes the exact path otherwise)
+__device__ __forceinline__ float pl_fatan2(float y, float x)
+{
+    const float ax = fabsf(x), ay = fabsf(y);
+    float r = ay > ax ? 1.5707963f - pl_fatan01(ax / ay) : pl_fatan01(ay / ax);
+    if (x < 0.0f) r = 3.1415927f - r;
+    return y < 0.0f ? -r : r;
+}
+
+// the polar angle's two cell indices: possible_interval's start_cell and the pruning's own cell cw
+__device__ __forceinline__ void pl_theta_cells(double wx, double wy, int n, double min_theta, double max_theta,
+                                               double angle_inc, int &start_cell, int &cw)
+{
+    auto adj = [&](double th, int &fl) {
+        fl = 0;
+        if (th < min_theta) {
+            th += 2.0 * SDM_PI;
+            fl = 1;
+        }
+        if (th > max_theta) {
+            th -= 2.0 * SDM_PI;
+            fl |= 2;
+        }
+        return th;
+    };
+    auto sc = [&](double th) { return (int)((th - min_theta) / (max_theta - min_theta) * n); };
+    auto cc = [&](double th) { return angle_inc > 0.0 ? (int)((th - min_theta) / angle_inc) : 0; };
+    const float fx = (float)wx, fy = (float)wy;
+    if (fx != 0.0f && fy != 0.0f) {
+        const double a = (double)pl_fatan2(fy, fx);
+        // near +-pi the exact atan2 may sit on the other side of the cut: no bracket there
+        if (fabs(a) <= SDM_PI - 4.0 * PL_ATAN_EPS) {
+            int fl0, fl1;
+            const double t0 = adj(a - PL_ATAN_EPS, fl0), t1 = adj(a + PL_ATAN_EPS, fl1);
+            const int s0 = sc(t0), c0 = cc(t0);
+            if (fl0 == fl1 && s0 == sc(t1) && c0 == cc(t1)) {
+                start_cell = s0;
+                cw = c0;
+                return;
+            }
+        }
+    }
+    int fl;
+    const double th = adj(sdm_atan2(wy, wx), fl);
+    start_cell = sc(th);
+    cw = cc(th);
+}
+
+// ceil(atan(u) / step) for u >= 0, the same bracket (k0 = the caller's constant term inside the ceil)
+__device__ __forceinline__ int pl_atan_cells(double u, double k0, double step)
+{
+    const double a = (double)pl_fatan((float)u);
+    if (a <= 2.0) {
+        const double lo = a - PL_ATAN_EPS > 0.0 ? a - PL_ATAN_EPS : 0.0, hi = a + PL_ATAN_EPS;
+        const int r0 = (int)ceil((k0 + lo) / step), r1 = (int)ceil((k0 + hi) / step);
+        if (r0 == r1) return r0;
+    }
+    return (int)ceil((k0 + sdm_atan(u)) / step);
+}
+
+// possible_interval (CSM icp_corr_dumb.c); also returns the point's own cell for the pruning
 __device__ __forceinline__ void pl_interval(const pl_params &p, double wx, double wy, int n, double min_theta,
-                                            double max_theta, int &from, int &to)
+                                            double max_theta, double angle_inc, int &from, int &to, int &cw)
 {
     const double angle_res = (max_theta - min_theta) / n;
     const double norm = sqrt(wx * wx + wy * wy);
-    const double delta = fabs(p.max_angular_correction_deg * (SDM_PI / 180.0)) + fabs(sdm_atan(p.max_linear_correction / norm));
-    const int range = (int)ceil(delta / angle_res);
-    double start_theta = sdm_atan2(wy, wx);
-    if (start_theta < min_theta) start_theta += 2.0 * SDM_PI;
-    if (start_theta > max_theta) start_theta -= 2.0 * SDM_PI;
-    const int start_cell = (int)((start_theta - min_theta) / (max_theta - min_theta) * n);
+    // delta = |max_angular_correction| + |atan(max_linear_correction / norm)|, range = ceil(delta / angle_res)
+    const int range = pl_atan_cells(p.max_linear_correction / norm, fabs(p.max_angular_correction_deg * (SDM_PI / 180.0)),
+                                    angle_res);
+    int start_cell;
+    pl_theta_cells(wx, wy, n, min_theta, max_theta, angle_inc, start_cell, cw);
     const int f = start_cell - range, t = start_cell + range;
     from = f < 0 ? 0 : (f > n - 1 ? n - 1 : f);
     to = t < 0 ? 0 : (t > n - 1 ? n - 1 : t);
@@ -335,8 +423,8 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
             if (i >= n || !sval[k]) continue;
             const double wx = (c * spx[k] - s * spy[k]) + x_old[0];   // ld_compute_world_coords
             const double wy = (s * spx[k] + c * spy[k]) + x_old[1];
-            int from, to;
-            pl_interval(p, wx, wy, n, min_theta, max_theta, from, to);
+            int from, to, cw;
+            pl_interval(p, wx, wy, n, min_theta, max_theta, angle_inc, from, to, cw);
             int b1 = -1;
             double best = 0.0;
             bool searched = false;
@@ -349,10 +437,7 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                 const double norm = sqrt(wx * wx + wy * wy);
                 const double lim = 1.01 * p.max_correspondence_dist;
                 if (norm > 2.0 * lim && angle_inc > 0.0) {
-                    double th = sdm_atan2(wy, wx);
-                    if (th < min_theta) th += 2.0 * SDM_PI;
-                    if (th > max_theta) th -= 2.0 * SDM_PI;
-                    const int cw = (int)((th - min_theta) / angle_inc);
+                    // cw = (int)((theta_w - min_theta) / angle_inc), theta_w adjusted as in possible_interval
                     // Tighter still: the best distance among the 9 cells around the point's own cell
                     // bounds the winner, so the same argument with lim = 1.01 sqrt(that) shrinks the
                     // window further (every point left out is > that distance, hence not the minimum).
@@ -372,18 +457,17 @@ pl_icp_kernel(pl_params p, int n, double angle_min, double angle_inc, const doub
                     }
                     if (b1 != -1) {
                         const double sn2 = 1.01 * sqrt(best) / norm;
-                        const double dth2 = sdm_atan(sn2 / sqrt(1.0 - sn2 * sn2));
-                        // a cell j with |j - cw| > m2 is at least m2 cells of angle away from w (w lies
-                        // inside cell cw), so ceil(dth2 / inc) would do; +1 covers cw's rounding, +1 margin
-                        const int m2 = (int)ceil(dth2 / angle_inc) + 2;
+                        // dth2 = atan(sn2 / sqrt(1 - sn2^2)): a cell j with |j - cw| > m2 is at least m2 cells
+                        // of angle away from w (w lies inside cell cw), so ceil(dth2 / inc) would do; +1
+                        // covers cw's rounding, +1 margin
+                        const int m2 = pl_atan_cells(sn2 / sqrt(1.0 - sn2 * sn2), 0.0, angle_inc) + 2;
                         from = from > cw - m2 ? from : cw - m2;
                         to = to < cw + m2 ? to : cw + m2;
                         if (from >= cf && to <= ct) searched = true;
                         else b1 = -1;
                     } else {
                         const double sn_ = lim / norm;
-                        const double dth = sdm_atan(sn_ / sqrt(1.0 - sn_ * sn_));
-                        const int m = (int)ceil(dth / angle_inc) + 3;
+                        const int m = pl_atan_cells(sn_ / sqrt(1.0 - sn_ * sn_), 0.0, angle_inc) + 3;
                         from = from > cw - m ? from : cw - m;
                         to = to < cw + m ? to : cw + m;
                     }

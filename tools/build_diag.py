@@ -13,6 +13,7 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   gmplain    WRONG RESULTS  gm_compute_kernel walks with plain LDS stores instead of atomicAdd
   gmnowalk   WRONG RESULTS  gm_compute_kernel clips every line to the tile but skips the walk
   nowalk     WRONG RESULTS  hs_update_kernel clips every ray to the tile but skips the Bresenham walk
+  plfastatan WRONG RESULTS  pl_icp_kernel uses float atan / atan2 (prices the exact double ones)
   nosetup    WRONG RESULTS  hs_update_kernel keeps the fan-group culling of every tile, skips every ray
   noraster   WRONG RESULTS  hs_update_kernel skips the raster loop (tile loop skeleton: clear, barriers)
 """
@@ -35,6 +36,9 @@ PATCHES = {
     "gmplain": [("gmapping_kernels.hip", "        atomicAdd(reinterpret_cast<unsigned *>(pc), 1u); /* visits++ (:227-234) */ \\\n",
                  "        *reinterpret_cast<volatile unsigned *>(pc) = 1u;                             \\\n")],
     "gmnowalk": [("gmapping_kernels.hip", "            int i = 0;\n#define GM_WSTEP", "            int i = steps;\n#define GM_WSTEP")],
+    "plfastatan": [("plicp_kernels.hip", '#include "detmath.h"\n',
+                    '#include "detmath.h"\n#define sdm_atan2(y, x) ((double)atan2f((float)(y), (float)(x)))\n'
+                    '#define sdm_atan(x) ((double)atanf((float)(x)))\n')],
     "nowalk": [(K, "                if (lo_i > hi_i) continue;\n                any = true;\n",
                 "                if (lo_i > hi_i) continue;\n                any = true;\n                continue;\n")],
     "nosetup": [(K, "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n",

@@ -529,6 +529,13 @@ constexpr int KT_AS_MARGIN = 16;       // LDS tile margin (footprints of kernel 
 constexpr int KT_AS_TW = 64 + 2 * KT_AS_MARGIN;
 constexpr int KT_AS_MAX_TILES = 2048;  // tiles per grid (e.g. 2896 x 2896 cells)
 constexpr int KT_AS_MAX_BASE = 1024;
+constexpr int KT_AS_CLASSES = 12;  // tile size classes of the render order
+
+__device__ __forceinline__ int kt_size_class(int c)  // 0 for c >= 2^11, 11 for c == 1
+{
+    const int lg = 31 - __builtin_clz((unsigned)c);
+    return lg >= KT_AS_CLASSES - 1 ? 0 : KT_AS_CLASSES - 1 - lg;
+}
 
 template <int NW>
 __device__ __forceinline__ int kt_block_exscan_n(int v, int *sw, int *total)
@@ -562,6 +569,68 @@ __device__ __forceinline__ int kt_tiles_of(int cx, int cy, int h, int tiles_x, i
     return c;
 }
 
+// One wave renders the items [c0, c1) of a tile into its LDS tile (fast path, ks <= KT_FAST_KS): lane
+// slot u < NS owns kernel cell lane + 64 u at byte offset koff[u] from the footprint's origin; slots
+// below NS - 1 are full, the last one is exec-masked to its owners (own_last).  The items are read 64 at
+// a time (one LDS read, then v_readlane per item).  Item j is paired with item j + half of the chunk:
+// when their footprints are disjoint, both are read before either is written (one LDS round trip for
+// the two); otherwise they run one after the other.  Byte max is order-free, so any order is exact.
+template <int NS>
+__device__ __forceinline__ void kt_render_items(unsigned char *tileb, const unsigned *sitem, int c0, int c1, int base,
+                                                int ks, const int (&koff)[4], const unsigned (&kv)[4], bool own_last)
+{
+    const int lane = threadIdx.x & 63;
+    auto one = [&](int o) {
+        unsigned cur[NS];
+#pragma unroll
+        for (int u = 0; u < NS - 1; ++u) cur[u] = tileb[koff[u] + o];
+#pragma unroll
+        for (int u = 0; u < NS - 1; ++u) tileb[koff[u] + o] = (unsigned char)max(cur[u], kv[u]);
+        if (own_last) {
+            const unsigned c = tileb[koff[NS - 1] + o];
+            tileb[koff[NS - 1] + o] = (unsigned char)max(c, kv[NS - 1]);
+        }
+    };
+    auto two = [&](int oa, int ob) {
+        unsigned ca[NS], cb[NS];
+#pragma unroll
+        for (int u = 0; u < NS - 1; ++u) {
+            ca[u] = tileb[koff[u] + oa];
+            cb[u] = tileb[koff[u] + ob];
+        }
+#pragma unroll
+        for (int u = 0; u < NS - 1; ++u) {
+            tileb[koff[u] + oa] = (unsigned char)max(ca[u], kv[u]);
+            tileb[koff[u] + ob] = (unsigned char)max(cb[u], kv[u]);
+        }
+        if (own_last) {
+            const unsigned a = tileb[koff[NS - 1] + oa], b = tileb[koff[NS - 1] + ob];
+            tileb[koff[NS - 1] + oa] = (unsigned char)max(a, kv[NS - 1]);
+            tileb[koff[NS - 1] + ob] = (unsigned char)max(b, kv[NS - 1]);
+        }
+    };
+    for (int cb = c0; cb < c1; cb += 64) {
+        const int ne = min(64, c1 - cb);
+        const int mine = lane < ne ? (int)sitem[cb + lane] : 0;
+        const int half = ne >> 1;
+        for (int j = 0; j < half; ++j) {
+            const int a = __builtin_amdgcn_readlane(mine, j), b = __builtin_amdgcn_readlane(mine, j + half);
+            const int ax = a & 0xFFFF, ay = a >> 16, bx = b & 0xFFFF, by = b >> 16;
+            const int oa = base + ay * KT_AS_TW + ax, ob = base + by * KT_AS_TW + bx;  // scalar
+            if (abs(ax - bx) >= ks || abs(ay - by) >= ks) {
+                two(oa, ob);
+            } else {
+                one(oa);
+                one(ob);
+            }
+        }
+        if (ne & 1) {
+            const int a = __builtin_amdgcn_readlane(mine, ne - 1);
+            one(base + (a >> 16) * KT_AS_TW + (a & 0xFFFF));
+        }
+    }
+}
+
 __global__ void __launch_bounds__(KT_AS_WAVES * 64)
 kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int *__restrict__ bbeg,
                    const int *__restrict__ bidx, const unsigned char *__restrict__ kernel, unsigned char *grids,
@@ -575,7 +644,8 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
     __shared__ unsigned long long stile[KT_AS_WAVES][KT_AS_TW * KT_AS_TW / 8 + 8];  // + 64 trash bytes
     __shared__ unsigned char sk[41 * 41];
     __shared__ int sw[KT_AS_WAVES];
-    __shared__ int s_ndirty, s_pass_end;
+    __shared__ int s_ndirty, s_pass_end, s_next;
+    __shared__ int sbk[2 * KT_AS_CLASSES + 1];  // per size class: list offset, cursor; then the list length
     constexpr int NT = KT_AS_WAVES * 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int m = blockIdx.x;
@@ -591,7 +661,10 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
     for (int i = tid; i < ks * ks; i += NT) sk[i] = kernel[i];
     for (int t = tid; t < NTL; t += NT) sdirty[t] = 0;
     for (int j = tid; j < nb; j += NT) sscan[j] = 0;
-    if (tid == 0) s_ndirty = 0;
+    if (tid == 0) {
+        s_ndirty = 0;
+        s_next = 0;
+    }
     __syncthreads();
     // ---- 1. cells of the valid in-ROI points ----
     for (int i = tid; i < nb * n; i += NT) {
@@ -623,18 +696,20 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
     }
     __syncthreads();
     KT_STAMP(1);
-    // per-lane kernel cells (ks <= 15: at most 4 of the <= 225 cells per lane)
-    int cell_dy[4], cell_dx[4];
-    unsigned char cell_kv[4];
+    // per-lane kernel cells (ks <= 15: at most 4 of the <= 225 cells per lane), as byte offsets in the
+    // LDS tile from the footprint's origin
+    int koff[4];
+    unsigned kvv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int t = lane + 64 * u;
         const int jj = t / ks, ii = t - jj * ks;
         const bool in = ks <= KT_FAST_KS && t < ks * ks;
-        cell_dy[u] = in ? jj : 0;
-        cell_dx[u] = in ? ii : 0;
-        cell_kv[u] = in ? sk[ii + ks * jj] : 0;
+        koff[u] = in ? jj * KT_AS_TW + ii : 0;
+        kvv[u] = in ? sk[ii + ks * jj] : 0u;
     }
+    const int nslot = (ks * ks + 63) >> 6;
+    const bool own_last = lane + 64 * (nslot - 1) < ks * ks;
     unsigned long long *tile = stile[wave];
     unsigned char *tileb = reinterpret_cast<unsigned char *>(tile);
     int pa = 0;
@@ -645,6 +720,7 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
             s_pass_end = pb;
         }
         for (int t = tid; t < NTL; t += NT) scur[t] = 0;
+        if (tid < 2 * KT_AS_CLASSES + 1) sbk[tid] = 0;
         __syncthreads();
         const int pb = s_pass_end;
         // ---- 2. count per tile, prefix, scatter tile-sorted ----
@@ -680,15 +756,47 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
             const int c = kt_tiles_of(cell & 0xFFFF, cell >> 16, h, g.tiles_x, tl);
             for (int q = 0; q < c; ++q) sitem[atomicAdd(&scur[tl[q]], 1)] = (unsigned)cell;
         }
+        // the tiles with items by size class (class 0: >= 2^(KT_AS_CLASSES - 1) items, then halving)
+        for (int t = tid; t < NTL; t += NT) {
+            const int c = soff[t + 1] - soff[t];
+            if (c) atomicAdd(&sbk[kt_size_class(c)], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int k = 0; k < KT_AS_CLASSES; ++k) {
+                const int v = sbk[k];
+                sbk[k] = acc;
+                acc += v;
+            }
+            sbk[2 * KT_AS_CLASSES] = acc;
+        }
+        __syncthreads();
+        // the scatter is done, so scur becomes the tile list, heaviest class first: the waves take tiles
+        // from it in turn (greedy largest-first; round-robin by tile index left one wave a third above
+        // the mean)
+        int *slist = scur;
+        for (int t = tid; t < NTL; t += NT) {
+            const int c = soff[t + 1] - soff[t];
+            if (c) {
+                const int k = kt_size_class(c);
+                slist[sbk[k] + atomicAdd(&sbk[KT_AS_CLASSES + k], 1)] = t;
+            }
+        }
         __syncthreads();
         if (pa == 0) KT_STAMP(3);
         // ---- 3. render whole tiles, plain stores ----
         // The LDS tile is the 64 x 64 tile plus a 16-cell margin on every side, so a footprint of any
         // point listed for the tile (kernel half <= 8 in this path) lies inside it: no bounds tests,
         // no divergence; cells a lane does not own get max(x, 0) = x written back.
-        for (int t = wave; t < NTL; t += KT_AS_WAVES) {
+        const int nlist = sbk[2 * KT_AS_CLASSES];
+        for (;;) {
+            int k = 0;
+            if (lane == 0) k = atomicAdd(&s_next, 1);
+            k = __builtin_amdgcn_readfirstlane(k);
+            if (k >= nlist) break;
+            const int t = __builtin_amdgcn_readfirstlane(slist[k]);
             const int c0 = soff[t], c1 = soff[t + 1];
-            if (c0 == c1) continue;
             const int ty = t / g.tiles_x, tx = t - ty * g.tiles_x;
             const int x0 = tx * 64, y0 = ty * 64;
             const bool was = sdirty[t] != 0;
@@ -700,26 +808,15 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
                         tile[((r + KT_AS_MARGIN) * KT_AS_TW + KT_AS_MARGIN) / 8 + (q & 7)] = gw[(size_t)y * wsw + xq];
                 }
             if (ks <= KT_FAST_KS) {
-                // A lane that owns no kernel cell in slot u (its kernel value is 0, so it writes back what it
-                // read) addresses byte (ks rows below the footprint's origin) + lane: outside the footprint's
-                // rows, so never a byte an owning lane of the same store writes, and inside the tile
-                // buffer (origin row <= 16 + 63, + 15 rows, + 142 bytes < 96 * 96 + 64).  Every address is
-                // then the scalar item origin plus a per-lane constant: one add per slot.
-                unsigned char *tb[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const bool own = lane + 64 * u < ks * ks;
-                    tb[u] = tileb + (own ? cell_dy[u] * KT_AS_TW + cell_dx[u] : ks * KT_AS_TW + lane);
-                }
+                // The LDS tile is the 64 x 64 tile plus a 16-cell margin on every side, so a footprint of
+                // any point listed for the tile (kernel half <= 8 in this path) lies inside it: no bounds
+                // tests.  base + (cell row) * TW + (cell col) is the footprint origin's byte (scalar).
                 const int base = __builtin_amdgcn_readfirstlane((KT_AS_MARGIN - h - y0) * KT_AS_TW + (KT_AS_MARGIN - h - x0));
-                for (int c = c0; c < c1; ++c) {
-                    const unsigned cell = (unsigned)__builtin_amdgcn_readfirstlane((int)sitem[c]);
-                    const int o = base + (int)(cell >> 16) * KT_AS_TW + (int)(cell & 0xFFFFu);  // scalar
-                    unsigned cur[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) cur[u] = tb[u][o];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) tb[u][o] = (unsigned char)max(cur[u], (unsigned)cell_kv[u]);
+                switch (nslot) {
+                case 1: kt_render_items<1>(tileb, sitem, c0, c1, base, ks, koff, kvv, own_last); break;
+                case 2: kt_render_items<2>(tileb, sitem, c0, c1, base, ks, koff, kvv, own_last); break;
+                case 3: kt_render_items<3>(tileb, sitem, c0, c1, base, ks, koff, kvv, own_last); break;
+                default: kt_render_items<4>(tileb, sitem, c0, c1, base, ks, koff, kvv, own_last); break;
                 }
             } else {
                 for (int c = c0; c < c1; ++c) {
@@ -746,6 +843,7 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
             }
         }
         __syncthreads();
+        if (tid == 0) s_next = 0;
         if (pa == 0) KT_STAMP(4);
         pa = pb;
     }

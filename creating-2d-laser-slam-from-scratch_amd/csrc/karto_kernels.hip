@@ -570,43 +570,36 @@ __device__ __forceinline__ int kt_tiles_of(int cx, int cy, int h, int tiles_x, i
 }
 
 // One wave renders the items [c0, c1) of a tile into its LDS tile (fast path, ks <= KT_FAST_KS): lane
-// slot u < NS owns kernel cell lane + 64 u at byte offset koff[u] from the footprint's origin; slots
-// below NS - 1 are full, the last one is exec-masked to its owners (own_last).  The items are read 64 at
-// a time (one LDS read, then v_readlane per item).  Item j is paired with item j + half of the chunk:
+// slot u < NS holds kernel cell (lane + 64 u) mod ks^2 at byte offset koff[u] from the footprint's
+// origin.  Lanes past the last cell duplicate a cell another slot (or lane) also holds, with the same
+// kernel value: both write max(old, kv) or max(max(old, kv), kv), the same byte, so every slot runs on
+// all lanes, unmasked and with no trash bytes.  The items are read 64 at a time (one LDS read, then
+// v_readlane per item).  Item j is paired with item j + half of the chunk:
 // when their footprints are disjoint, both are read before either is written (one LDS round trip for
 // the two); otherwise they run one after the other.  Byte max is order-free, so any order is exact.
 template <int NS>
 __device__ __forceinline__ void kt_render_items(unsigned char *tileb, const unsigned *sitem, int c0, int c1, int base,
-                                                int ks, const int (&koff)[4], const unsigned (&kv)[4], bool own_last)
+                                                int ks, const int (&koff)[4], const unsigned (&kv)[4])
 {
     const int lane = threadIdx.x & 63;
     auto one = [&](int o) {
         unsigned cur[NS];
 #pragma unroll
-        for (int u = 0; u < NS - 1; ++u) cur[u] = tileb[koff[u] + o];
+        for (int u = 0; u < NS; ++u) cur[u] = tileb[koff[u] + o];
 #pragma unroll
-        for (int u = 0; u < NS - 1; ++u) tileb[koff[u] + o] = (unsigned char)max(cur[u], kv[u]);
-        if (own_last) {
-            const unsigned c = tileb[koff[NS - 1] + o];
-            tileb[koff[NS - 1] + o] = (unsigned char)max(c, kv[NS - 1]);
-        }
+        for (int u = 0; u < NS; ++u) tileb[koff[u] + o] = (unsigned char)max(cur[u], kv[u]);
     };
     auto two = [&](int oa, int ob) {
         unsigned ca[NS], cb[NS];
 #pragma unroll
-        for (int u = 0; u < NS - 1; ++u) {
+        for (int u = 0; u < NS; ++u) {
             ca[u] = tileb[koff[u] + oa];
             cb[u] = tileb[koff[u] + ob];
         }
 #pragma unroll
-        for (int u = 0; u < NS - 1; ++u) {
+        for (int u = 0; u < NS; ++u) {
             tileb[koff[u] + oa] = (unsigned char)max(ca[u], kv[u]);
             tileb[koff[u] + ob] = (unsigned char)max(cb[u], kv[u]);
-        }
-        if (own_last) {
-            const unsigned a = tileb[koff[NS - 1] + oa], b = tileb[koff[NS - 1] + ob];
-            tileb[koff[NS - 1] + oa] = (unsigned char)max(a, kv[NS - 1]);
-            tileb[koff[NS - 1] + ob] = (unsigned char)max(b, kv[NS - 1]);
         }
     };
     for (int cb = c0; cb < c1; cb += 64) {
@@ -702,14 +695,13 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
     unsigned kvv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int t = lane + 64 * u;
+        const int t = (lane + 64 * u) % (ks * ks);  // past the last cell: a duplicate (kt_render_items)
         const int jj = t / ks, ii = t - jj * ks;
-        const bool in = ks <= KT_FAST_KS && t < ks * ks;
+        const bool in = ks <= KT_FAST_KS;
         koff[u] = in ? jj * KT_AS_TW + ii : 0;
         kvv[u] = in ? sk[ii + ks * jj] : 0u;
     }
     const int nslot = (ks * ks + 63) >> 6;
-    const bool own_last = lane + 64 * (nslot - 1) < ks * ks;
     unsigned long long *tile = stile[wave];
     unsigned char *tileb = reinterpret_cast<unsigned char *>(tile);
     int pa = 0;
@@ -813,10 +805,10 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
                 // tests.  base + (cell row) * TW + (cell col) is the footprint origin's byte (scalar).
                 const int base = __builtin_amdgcn_readfirstlane((KT_AS_MARGIN - h - y0) * KT_AS_TW + (KT_AS_MARGIN - h - x0));
                 switch (nslot) {
-                case 1: kt_render_items<1>(tileb, sitem, c0, c1, base, ks, koff, kvv, own_last); break;
-                case 2: kt_render_items<2>(tileb, sitem, c0, c1, base, ks, koff, kvv, own_last); break;
-                case 3: kt_render_items<3>(tileb, sitem, c0, c1, base, ks, koff, kvv, own_last); break;
-                default: kt_render_items<4>(tileb, sitem, c0, c1, base, ks, koff, kvv, own_last); break;
+                case 1: kt_render_items<1>(tileb, sitem, c0, c1, base, ks, koff, kvv); break;
+                case 2: kt_render_items<2>(tileb, sitem, c0, c1, base, ks, koff, kvv); break;
+                case 3: kt_render_items<3>(tileb, sitem, c0, c1, base, ks, koff, kvv); break;
+                default: kt_render_items<4>(tileb, sitem, c0, c1, base, ks, koff, kvv); break;
                 }
             } else {
                 for (int c = c0; c < c1; ++c) {

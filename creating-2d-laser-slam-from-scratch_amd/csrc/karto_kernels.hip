@@ -624,6 +624,59 @@ __device__ __forceinline__ void kt_render_items(unsigned char *tileb, const unsi
     }
 }
 
+// Dword form of the render for kernels up to KT_DW_KS wide: a footprint row of ks bytes starting at
+// any byte lies in 4 aligned dwords, so lane (r, k) of the first ks * nd lanes owns aligned dword k of
+// footprint row r (nd = dwords per row), one ds_read_b32 + one ds_write_b32 per item.  Its 4 kernel
+// bytes depend on the origin's alignment s: they are bytes 3 - s .. 6 - s of the lane's 8 bytes of the
+// row's kernel padded with 3 leading zeros (klo, khi), one v_alignbyte.  Bytes outside the footprint
+// get kernel 0 (max(x, 0) = x), lanes past ks * nd duplicate a lane's dword (same value written), and a
+// pair is rendered together only when the dword spans are disjoint.  Byte max is per-byte SWAR, exact
+// because every grid byte and kernel value is <= 100 < 128.
+constexpr int KT_DW_KS = 13;
+
+__device__ __forceinline__ unsigned kt_bytemax7(unsigned a, unsigned b)
+{
+    const unsigned t = ((a | 0x80808080u) - b) & 0x80808080u;  // 0x80 in every byte where a >= b
+    return b ^ ((a ^ b) & (t - (t >> 7)));
+}
+
+__device__ __forceinline__ void kt_render_items_dw(unsigned char *tileb, const unsigned *sitem, int c0, int c1, int bx,
+                                                   int by, int ks, int nd, int koffd, unsigned klo, unsigned khi)
+{
+    const int lane = threadIdx.x & 63;
+    auto one = [&](int row, int col) {
+        unsigned *w = reinterpret_cast<unsigned *>(tileb + row * KT_AS_TW + (col & ~3) + koffd);
+        const unsigned kv = __builtin_amdgcn_alignbyte(khi, klo, 3 - (col & 3));
+        const unsigned x = *w;
+        *w = kt_bytemax7(x, kv);
+    };
+    for (int cb = c0; cb < c1; cb += 64) {
+        const int ne = min(64, c1 - cb);
+        const int mine = lane < ne ? (int)sitem[cb + lane] : 0;
+        const int half = ne >> 1;
+        for (int j = 0; j < half; ++j) {
+            const int a = __builtin_amdgcn_readlane(mine, j), b = __builtin_amdgcn_readlane(mine, j + half);
+            const int ra = by + (a >> 16), ca = bx + (a & 0xFFFF), rb = by + (b >> 16), cb2 = bx + (b & 0xFFFF);
+            if (abs(ra - rb) >= ks || abs((ca >> 2) - (cb2 >> 2)) >= nd) {
+                unsigned *wa = reinterpret_cast<unsigned *>(tileb + ra * KT_AS_TW + (ca & ~3) + koffd);
+                unsigned *wb = reinterpret_cast<unsigned *>(tileb + rb * KT_AS_TW + (cb2 & ~3) + koffd);
+                const unsigned ka = __builtin_amdgcn_alignbyte(khi, klo, 3 - (ca & 3));
+                const unsigned kb = __builtin_amdgcn_alignbyte(khi, klo, 3 - (cb2 & 3));
+                const unsigned xa = *wa, xb = *wb;
+                *wa = kt_bytemax7(xa, ka);
+                *wb = kt_bytemax7(xb, kb);
+            } else {
+                one(ra, ca);
+                one(rb, cb2);
+            }
+        }
+        if (ne & 1) {
+            const int a = __builtin_amdgcn_readlane(mine, ne - 1);
+            one(by + (a >> 16), bx + (a & 0xFFFF));
+        }
+    }
+}
+
 __global__ void __launch_bounds__(KT_AS_WAVES * 64)
 kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int *__restrict__ bbeg,
                    const int *__restrict__ bidx, const unsigned char *__restrict__ kernel, unsigned char *grids,
@@ -702,6 +755,22 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
         kvv[u] = in ? sk[ii + ks * jj] : 0u;
     }
     const int nslot = (ks * ks + 63) >> 6;
+    // dword form (ks <= KT_DW_KS): lane -> (row r, dword k), klo / khi = padded kernel bytes 4k .. 4k + 7
+    const int nd = (ks + 6) >> 2;
+    int koffd = 0;
+    unsigned klo = 0u, khi = 0u;
+    if (ks <= KT_DW_KS) {
+        const int t = lane % (ks * nd);
+        const int r = t / nd, k = t - r * nd;
+        koffd = r * KT_AS_TW + 4 * k;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = 4 * k + j - 3;
+            const unsigned v = (c >= 0 && c < ks) ? (unsigned)sk[c + ks * r] : 0u;
+            if (j < 4) klo |= v << (8 * j);
+            else khi |= v << (8 * (j - 4));
+        }
+    }
     unsigned long long *tile = stile[wave];
     unsigned char *tileb = reinterpret_cast<unsigned char *>(tile);
     int pa = 0;
@@ -799,7 +868,10 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
                     if (y < g.height && xq < wsw)
                         tile[((r + KT_AS_MARGIN) * KT_AS_TW + KT_AS_MARGIN) / 8 + (q & 7)] = gw[(size_t)y * wsw + xq];
                 }
-            if (ks <= KT_FAST_KS) {
+            if (ks <= KT_DW_KS) {
+                kt_render_items_dw(tileb, sitem, c0, c1, KT_AS_MARGIN - h - x0, KT_AS_MARGIN - h - y0, ks, nd, koffd, klo,
+                                   khi);
+            } else if (ks <= KT_FAST_KS) {
                 // The LDS tile is the 64 x 64 tile plus a 16-cell margin on every side, so a footprint of
                 // any point listed for the tile (kernel half <= 8 in this path) lies inside it: no bounds
                 // tests.  base + (cell row) * TW + (cell col) is the footprint origin's byte (scalar).

@@ -605,6 +605,7 @@ __device__ __forceinline__ void kt_render_items(unsigned char *tileb, const unsi
     for (int cb = c0; cb < c1; cb += 64) {
         const int ne = min(64, c1 - cb);
         const int mine = lane < ne ? (int)sitem[cb + lane] : 0;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), as in kt_render_items_dw
         const int half = ne >> 1;
         for (int j = 0; j < half; ++j) {
             const int a = __builtin_amdgcn_readlane(mine, j), b = __builtin_amdgcn_readlane(mine, j + half);
@@ -629,9 +630,9 @@ __device__ __forceinline__ void kt_render_items(unsigned char *tileb, const unsi
 // footprint row r (nd = dwords per row), one ds_read_b32 + one ds_write_b32 per item.  Its 4 kernel
 // bytes depend on the origin's alignment s: they are bytes 3 - s .. 6 - s of the lane's 8 bytes of the
 // row's kernel padded with 3 leading zeros (klo, khi), one v_alignbyte.  Bytes outside the footprint
-// get kernel 0 (max(x, 0) = x), lanes past ks * nd duplicate a lane's dword (same value written), and a
-// pair is rendered together only when the dword spans are disjoint.  Byte max is per-byte SWAR, exact
-// because every grid byte and kernel value is <= 100 < 128.
+// get kernel 0 (max(x, 0) = x) and lanes past ks * nd duplicate a lane's dword (same value written).
+// Items run one after the other (pairs with disjoint dword spans read before either write measured
+// slower here).  Byte max is per-byte SWAR, exact because every grid byte and kernel value is <= 100.
 constexpr int KT_DW_KS = 13;
 
 __device__ __forceinline__ unsigned kt_bytemax7(unsigned a, unsigned b)
@@ -653,25 +654,11 @@ __device__ __forceinline__ void kt_render_items_dw(unsigned char *tileb, const u
     for (int cb = c0; cb < c1; cb += 64) {
         const int ne = min(64, c1 - cb);
         const int mine = lane < ne ? (int)sitem[cb + lane] : 0;
-        const int half = ne >> 1;
-        for (int j = 0; j < half; ++j) {
-            const int a = __builtin_amdgcn_readlane(mine, j), b = __builtin_amdgcn_readlane(mine, j + half);
-            const int ra = by + (a >> 16), ca = bx + (a & 0xFFFF), rb = by + (b >> 16), cb2 = bx + (b & 0xFFFF);
-            if (abs(ra - rb) >= ks || abs((ca >> 2) - (cb2 >> 2)) >= nd) {
-                unsigned *wa = reinterpret_cast<unsigned *>(tileb + ra * KT_AS_TW + (ca & ~3) + koffd);
-                unsigned *wb = reinterpret_cast<unsigned *>(tileb + rb * KT_AS_TW + (cb2 & ~3) + koffd);
-                const unsigned ka = __builtin_amdgcn_alignbyte(khi, klo, 3 - (ca & 3));
-                const unsigned kb = __builtin_amdgcn_alignbyte(khi, klo, 3 - (cb2 & 3));
-                const unsigned xa = *wa, xb = *wb;
-                *wa = kt_bytemax7(xa, ka);
-                *wb = kt_bytemax7(xb, kb);
-            } else {
-                one(ra, ca);
-                one(rb, cb2);
-            }
-        }
-        if (ne & 1) {
-            const int a = __builtin_amdgcn_readlane(mine, ne - 1);
+        // wait for the item read here: left to the compiler, the wait lands inside the loop, where it
+        // also waits for every item's store before the next item's load is issued
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        for (int j = 0; j < ne; ++j) {
+            const int a = __builtin_amdgcn_readlane(mine, j);
             one(by + (a >> 16), bx + (a & 0xFFFF));
         }
     }

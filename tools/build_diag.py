@@ -16,6 +16,8 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   plfastatan WRONG RESULTS  pl_icp_kernel uses float atan / atan2 (prices the exact double ones)
   nosetup    WRONG RESULTS  hs_update_kernel keeps the fan-group culling of every tile, skips every ray
   noraster   WRONG RESULTS  hs_update_kernel skips the raster loop (tile loop skeleton: clear, barriers)
+  ktnorender WRONG RESULTS  kt_addscans_kernel clears, loads and stores its tiles but renders no item
+  ktnoswar   WRONG RESULTS  kt_addscans_kernel dword render writes the kernel bytes without the byte max
 """
 import os
 import shutil
@@ -44,6 +46,8 @@ PATCHES = {
     "nosetup": [(K, "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n",
                  "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n                continue;\n")],
     "noraster": [(K, "                const int4 gb = gbox[b0 >> 6];\n", "                if (b0 >= 0) break;\n                const int4 gb = gbox[b0 >> 6];\n")],
+    "ktnorender": [("karto_kernels.hip", "kt_render_items_dw(tileb, sitem, c0, c1,", "kt_render_items_dw(tileb, sitem, c0, c0,")],
+    "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 
 

@@ -700,31 +700,58 @@ kt_addscans_kernel(KtGeom g, KtPool P, const KtState *__restrict__ st, const int
     }
     __syncthreads();
     // ---- 1. cells of the valid in-ROI points ----
-    for (int i = tid; i < nb * n; i += NT) {
-        const int j = i / n, k = i - j * n;
-        const int s = bidx[jlo + j];
-        int cell = -1;
-        if (k < P.npts[s]) {
-            const double2 *pts = P.pts + (size_t)s * n;
-            const int2 e = P.evt[(size_t)s * n + k];
-            if (e.x >= 0) {
-                const double2 f = pts[e.y], cu = pts[e.x];
+    // four points per thread and trip, every load of the four issued before any is used (the chain
+    // bidx -> npts / evt -> pts is three dependent loads; out-of-range lanes read in-bounds index 0)
+    constexpr int KT_P1_U = 4;
+    for (int i0 = tid; i0 < nb * n; i0 += KT_P1_U * NT) {
+        int jv[KT_P1_U], kv[KT_P1_U], sv[KT_P1_U];
+#pragma unroll
+        for (int u = 0; u < KT_P1_U; ++u) {
+            const int i = i0 + u * NT;
+            const int ic = i < nb * n ? i : 0;
+            jv[u] = ic / n;
+            kv[u] = ic - jv[u] * n;
+            sv[u] = bidx[jlo + jv[u]];
+        }
+        int np[KT_P1_U];
+        int2 ev[KT_P1_U];
+#pragma unroll
+        for (int u = 0; u < KT_P1_U; ++u) {
+            np[u] = P.npts[sv[u]];
+            ev[u] = P.evt[(size_t)sv[u] * n + kv[u]];
+        }
+        double2 fv[KT_P1_U], cv[KT_P1_U], pv[KT_P1_U];
+        bool ok[KT_P1_U];
+#pragma unroll
+        for (int u = 0; u < KT_P1_U; ++u) {
+            const double2 *pts = P.pts + (size_t)sv[u] * n;
+            ok[u] = i0 + u * NT < nb * n && kv[u] < np[u] && ev[u].x >= 0;
+            fv[u] = pts[ok[u] ? ev[u].y : 0];
+            cv[u] = pts[ok[u] ? ev[u].x : 0];
+            pv[u] = pts[kv[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < KT_P1_U; ++u) {
+            const int i = i0 + u * NT;
+            if (i >= nb * n) break;
+            int cell = -1;
+            if (ok[u]) {
+                const double2 f = fv[u], cu = cv[u];
                 const double a = vy - f.y;
                 const double b = f.x - vx;
                 const double cc = f.y * vx - f.x * vy;
                 const double ss = cu.x * a + cu.y * b + cc;
                 if (!(ss < 0.0)) {  // wrong side of the viewpoint otherwise (Mapper.cpp:795-799)
-                    const double2 p = pts[k];
-                    const int gx = kt_w2g(p.x, gox, g.scale), gy = kt_w2g(p.y, goy, g.scale);
+                    const int gx = kt_w2g(pv[u].x, gox, g.scale), gy = kt_w2g(pv[u].y, goy, g.scale);
                     if (gx >= 0 && gx < g.grid_size && gy >= 0 && gy < g.grid_size)
                         cell = (gx + g.border) | ((gy + g.border) << 16);
                 }
             }
-        }
-        cellv[i] = cell;
-        if (cell >= 0) {
-            int tl[4];
-            atomicAdd(&sscan[j], kt_tiles_of(cell & 0xFFFF, cell >> 16, h, g.tiles_x, tl));
+            cellv[i] = cell;
+            if (cell >= 0) {
+                int tl[4];
+                atomicAdd(&sscan[jv[u]], kt_tiles_of(cell & 0xFFFF, cell >> 16, h, g.tiles_x, tl));
+            }
         }
     }
     __syncthreads();

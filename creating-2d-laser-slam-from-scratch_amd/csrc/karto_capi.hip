@@ -247,7 +247,7 @@ int kt_chunk_finish(kt_ctx *c, int count, const int *d_bbeg, const int *d_bidx, 
     const KtGeom &g = c->g;
     const int groups = (count + 7) / 8;
     if (refine)
-        KT_LAUNCH(K_FINE, kt_fine_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->pool(), c->d_state, c->d_grids,
+        KT_LAUNCH(K_FINE, kt_fine_kernel, dim3(count), dim3(KT_FINE_THREADS), 0, s, g, c->pool(), c->d_state, c->d_grids,
                   penalize, d_res);
     if (c->max_base > 0 && binned)
         KT_LAUNCH(K_CLEAR, kt_clear_tiles_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->d_grids, c->d_dirty,

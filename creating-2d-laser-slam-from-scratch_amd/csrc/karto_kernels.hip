@@ -1404,7 +1404,14 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
 
 // =================================================================================================
 // kt_fine_kernel: fine CorrelateScan + ComputeAngularCovariance, one workgroup per match
+//
+// Each thread holds its points (k = tid + u * KT_THREADS, up to KT_FINE_PPT) in registers for every
+// angle, the angles' sin / cos are computed once into LDS, and every angle's counts go to LDS by one
+// atomic add per wave (integer sums, order-free): no barrier between angles, and four points' offsets
+// and gathers (36 bytes) in flight per lane instead of one point's.
 // =================================================================================================
+constexpr int KT_FINE_THREADS = KT_THREADS;  // 1024 threads (4 waves per SIMD) measured slower
+constexpr int KT_FINE_PPT = 16;              // points per thread held in registers: n <= 4096 = 16 * 256
 __device__ __forceinline__ int kt_offset(const KtGeom &g, double cs, double sn, double2 l, double gox, double goy)
 {
     const double ox = cs * l.x - sn * l.y;
@@ -1412,12 +1419,13 @@ __device__ __forceinline__ int kt_offset(const KtGeom &g, double cs, double sn, 
     return kt_w2g(ox + gox, gox, g.scale) + kt_w2g(oy + goy, goy, g.scale) * g.ws;
 }
 
-__global__ void __launch_bounds__(KT_THREADS)
+__global__ void __launch_bounds__(KT_FINE_THREADS)
 kt_fine_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict__ grids, int penalize,
                kt_result *out)
 {
     __shared__ unsigned scnt[KT_FINE_MAX_ANG][9];
-    __shared__ unsigned sred[4][9];
+    __shared__ unsigned scov[KT_FINE_MAX_ANG];
+    __shared__ double s_cs[KT_FINE_MAX_ANG][2];
     __shared__ double sresp[KT_FINE_MAX_ANG * 9];
     __shared__ double s_mean[3];
     __shared__ double s_best;
@@ -1446,39 +1454,59 @@ kt_fine_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict_
         if (gx < 0 || gx >= g.width || gy < 0 || gy >= g.height) err = 1;
         gpos[p] = gx + gy * g.ws;
     }
-    for (int a = 0; a < nA; ++a) {
+    for (int i = tid; i < nA * 9; i += KT_FINE_THREADS) scnt[i / 9][i % 9] = 0u;
+    for (int a = tid; a < nA; a += KT_FINE_THREADS) {
         const double angle = astart + (double)(uint32_t)a * g.fares;
-        const double cs = sdm_cos(angle), sn = sdm_sin(angle);
+        s_cs[a][0] = sdm_cos(angle);
+        s_cs[a][1] = sdm_sin(angle);
+        scov[a] = 0u;
+    }
+    double2 lp[KT_FINE_PPT];
+    bool ok[KT_FINE_PPT];
+#pragma unroll
+    for (int u = 0; u < KT_FINE_PPT; ++u) {
+        const int k = tid + u * KT_FINE_THREADS;
+        ok[u] = k < npts && !bad[k];
+        lp[u] = ok[u] ? loc[k] : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+    for (int a = 0; a < nA; ++a) {
+        const double cs = s_cs[a][0], sn = s_cs[a][1];
         unsigned c[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int k = tid; k < npts; k += KT_THREADS) {
-            if (bad[k]) continue;
-            const int o = kt_offset(g, cs, sn, loc[k], gox, goy);
-            // branch-free: out-of-range cells read cell 0 and count 0, so all 9 gathers are in flight
-            unsigned char v[9];
 #pragma unroll
-            for (int p = 0; p < 9; ++p) {
-                const int idx = gpos[p] + o;
-                v[p] = grid[(unsigned)idx < ds ? idx : 0];
+        for (int u0 = 0; u0 < KT_FINE_PPT; u0 += 4) {
+            if (u0 * KT_FINE_THREADS >= npts) break;  // block-uniform
+            int o[4];
+            unsigned char v[4][9];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                o[u] = kt_offset(g, cs, sn, lp[u0 + u], gox, goy);
+                // branch-free: out-of-range cells read cell 0 and count 0, so all gathers are in flight
+#pragma unroll
+                for (int p = 0; p < 9; ++p) {
+                    const int idx = gpos[p] + o[u];
+                    v[u][p] = grid[(unsigned)idx < ds ? idx : 0];
+                }
             }
 #pragma unroll
-            for (int p = 0; p < 9; ++p) {
-                const int idx = gpos[p] + o;
-                c[p] += (unsigned)idx < ds ? v[p] : 0u;
-            }
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int p = 0; p < 9; ++p) {
+                    const int idx = gpos[p] + o[u];
+                    c[p] += (ok[u0 + u] && (unsigned)idx < ds) ? v[u][p] : 0u;
+                }
         }
 #pragma unroll
         for (int p = 0; p < 9; ++p) {
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) c[p] += __shfl_xor(c[p], off, 64);
-            if (lane == 0) sred[wave][p] = c[p];
+            if (lane == 0) atomicAdd(&scnt[a][p], c[p]);
         }
-        __syncthreads();
-        if (tid < 9) scnt[a][tid] = sred[0][tid] + sred[1][tid] + sred[2][tid] + sred[3][tid];
-        __syncthreads();
     }
+    __syncthreads();
     // responses in pose order (y, x, angle)
     const int np = 9 * nA;
-    for (int i = tid; i < np; i += KT_THREADS) {
+    for (int i = tid; i < np; i += KT_FINE_THREADS) {
         const int a = i % nA, p = i / nA;
         double response = 0.0;
         if (npts > 0) response = (double)scnt[a][p] / (double)(uint32_t)(npts * KT_OCC);
@@ -1532,20 +1560,24 @@ kt_fine_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict_
     // ComputeAngularCovariance: GetResponse at the best pose for every fine angle
     const int gi = s_gi;
     for (int a = 0; a < nA; ++a) {
-        const double angle = astart + (double)(uint32_t)a * g.fares;
-        const double cs = sdm_cos(angle), sn = sdm_sin(angle);
+        const double cs = s_cs[a][0], sn = s_cs[a][1];
         unsigned c = 0;
-        for (int k = tid; k < npts; k += KT_THREADS) {
-            if (bad[k]) continue;
-            const int idx = gi + kt_offset(g, cs, sn, loc[k], gox, goy);
-            if ((unsigned)idx < ds) c += grid[idx];
+#pragma unroll
+        for (int u0 = 0; u0 < KT_FINE_PPT; u0 += 4) {
+            if (u0 * KT_FINE_THREADS >= npts) break;  // block-uniform
+            int idx[4];
+            unsigned char v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                idx[u] = gi + kt_offset(g, cs, sn, lp[u0 + u], gox, goy);
+                v[u] = grid[(unsigned)idx[u] < ds ? idx[u] : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c += (ok[u0 + u] && (unsigned)idx[u] < ds) ? v[u] : 0u;
         }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
-        if (lane == 0) sred[wave][0] = c;
-        __syncthreads();
-        if (tid == 0) scnt[a][0] = sred[0][0] + sred[1][0] + sred[2][0] + sred[3][0];
-        __syncthreads();
+        if (lane == 0) atomicAdd(&scov[a], c);
     }
     if (err) S.status = KT_ERANGE;
     __syncthreads();
@@ -1555,7 +1587,7 @@ kt_fine_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict_
         double norm = 0.0, acc = 0.0;
         for (int a = 0; a < nA; ++a) {
             const double angle = astart + (double)(uint32_t)a * g.fares;
-            const double response = npts > 0 ? (double)scnt[a][0] / (double)(uint32_t)(npts * KT_OCC) : 0.0;
+            const double response = npts > 0 ? (double)scov[a] / (double)(uint32_t)(npts * KT_OCC) : 0.0;
             if (response >= (best - 0.1)) {
                 norm += response;
                 acc += (kt_sq(angle - best_angle) * response);

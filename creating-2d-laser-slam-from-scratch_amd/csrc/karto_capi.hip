@@ -191,7 +191,7 @@ int kt_end_event(kt_ctx *c, hipStream_t s, int which, std::pair<hipEvent_t, hipE
 
 int kt_prepare(kt_ctx *c, int first, int count, hipStream_t s)
 {
-    const size_t shm = (size_t)c->g.n * (sizeof(double2) + sizeof(int));
+    const size_t shm = (size_t)c->g.n * (sizeof(double2) + 2 * sizeof(int));
     KT_LAUNCH(K_PREPARE, kt_prepare_kernel, dim3(count), dim3(KT_THREADS), shm, s, c->g, c->pool(), first);
     return KT_OK;
 }
@@ -250,7 +250,7 @@ int kt_chunk_finish(kt_ctx *c, int count, const int *d_bbeg, const int *d_bidx, 
         KT_LAUNCH(K_FINE, kt_fine_kernel, dim3(count), dim3(KT_FINE_THREADS), 0, s, g, c->pool(), c->d_state, c->d_grids,
                   penalize, d_res);
     if (c->max_base > 0 && binned)
-        KT_LAUNCH(K_CLEAR, kt_clear_tiles_kernel, dim3(count), dim3(KT_THREADS), 0, s, g, c->d_grids, c->d_dirty,
+        KT_LAUNCH(K_CLEAR, kt_clear_tiles_kernel, dim3(count, 4), dim3(KT_THREADS), 0, s, g, c->d_grids, c->d_dirty,
                   c->d_dirty_cnt);
     else if (c->max_base > 0)
         KT_LAUNCH(K_CLEAR, (kt_build_kernel<1, 4>), dim3(groups * 8 * c->max_base), dim3(KT_THREADS), 0, s, g,
@@ -416,7 +416,7 @@ int kt_create(kt_ctx **out, const kt_laser *laser, const kt_params *params, int 
     }
 #undef KALLOC
     {
-        const size_t shm = (size_t)g.n * (sizeof(double2) + sizeof(int));
+        const size_t shm = (size_t)g.n * (sizeof(double2) + 2 * sizeof(int));
         if (shm > 65536 && (e = hipFuncSetAttribute((const void *)kt_prepare_kernel,
                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm)) != hipSuccess) {
             kt_destroy(c);

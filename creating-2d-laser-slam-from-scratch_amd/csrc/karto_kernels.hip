@@ -185,6 +185,7 @@ kt_prepare_kernel(KtGeom g, KtPool P, int first)
     extern __shared__ __attribute__((aligned(16))) unsigned char kt_smem[];
     double2 *spts = reinterpret_cast<double2 *>(kt_smem);       // [n]
     int *sev = reinterpret_cast<int *>(spts + g.n);              // [n] reset events
+    int *snext = sev + g.n;                                      // [n] next point beyond 0.1 m
     __shared__ int sw[4];
     __shared__ int s_nev;
 
@@ -230,22 +231,26 @@ kt_prepare_kernel(KtGeom g, KtPool P, int first)
     }
     if (tid == 0) P.npts[s] = npts;
     __syncthreads();
-    // FindValidPoints' reset events (the viewpoint-independent walk), one lane
-    if (tid == 0) {
-        const double min_sq = 0.1 * 0.1;
-        int nev = 0;
-        if (npts > 0) {
-            double fx = spts[0].x, fy = spts[0].y;
-            for (int j = 0; j < npts; ++j) {
-                const double2 c = spts[j];
-                const double dx = fx - c.x, dy = fy - c.y;
-                if (dx * dx + dy * dy > min_sq) {
-                    sev[nev++] = j;
-                    fx = c.x;
-                    fy = c.y;
-                }
-            }
+    // FindValidPoints' reset events (the viewpoint-independent walk): the walk keeps an anchor point and
+    // resets it at the first later point farther than 0.1 m from it.  next(j) = that point for anchor j
+    // (the same squared-distance test), found for every j in parallel; one lane then follows the chain
+    // 0 -> next(0) -> ..., one LDS read per event instead of one per point.
+    const double min_sq = 0.1 * 0.1;
+    for (int j = tid; j < npts; j += KT_THREADS) {
+        const double fx = spts[j].x, fy = spts[j].y;
+        int nx = j + 1;
+        for (; nx < npts; ++nx) {
+            const double2 c = spts[nx];
+            const double dx = fx - c.x, dy = fy - c.y;
+            if (dx * dx + dy * dy > min_sq) break;
         }
+        snext[j] = nx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int nev = 0;
+        if (npts > 0)
+            for (int a = snext[0]; a < npts; a = snext[a]) sev[nev++] = a;
         s_nev = nev;
     }
     __syncthreads();
@@ -938,7 +943,8 @@ kt_clear_tiles_kernel(KtGeom g, unsigned char *grids, const int *__restrict__ di
     const int cnt = dirty_count[m];
     const int wsw = g.ws >> 3;
     unsigned long long *gw = reinterpret_cast<unsigned long long *>(grids + (size_t)m * g.grid_stride);
-    for (int i = threadIdx.x; i < cnt * 512; i += KT_THREADS) {
+    // gridDim.y workgroups per match share its tiles (more stores in flight than one workgroup's)
+    for (int i = threadIdx.x + blockIdx.y * KT_THREADS; i < cnt * 512; i += KT_THREADS * gridDim.y) {
         const int t = dirty_list[(size_t)m * g.ntiles + (i >> 9)];
         const int q = i & 511;
         const int ty = t / g.tiles_x, tx = t - ty * g.tiles_x;

@@ -266,7 +266,11 @@ int kt_run_chunk(kt_ctx *c, int count, const int *d_query, const int *d_bbeg, co
     if (rc != KT_OK) return rc;
     for (int pass = 0; pass < c->g.npass; ++pass) {
         if ((rc = kt_chunk_coarse(c, count, pass, penalize, 0, 1, s)) != KT_OK) return rc;
-        KT_LAUNCH(K_SELECT, kt_select_kernel, dim3(count), dim3(KT_THREADS), 0, s, c->g, c->d_state, c->d_resp,
+        if (c->g.nxy * c->g.nxy > 512)
+            KT_LAUNCH(K_SELECT, kt_select_kernel<1024>, dim3(count), dim3(1024), 0, s, c->g, c->d_state, c->d_resp,
+                  c->d_posmax, c->d_tie_idx, c->d_tie_val, pass, refine, d_res);
+        else
+            KT_LAUNCH(K_SELECT, kt_select_kernel<KT_THREADS>, dim3(count), dim3(KT_THREADS), 0, s, c->g, c->d_state, c->d_resp,
                   c->d_posmax, c->d_tie_idx, c->d_tie_val, pass, refine, d_res);
     }
     return kt_chunk_finish(c, count, d_bbeg, d_bidx, penalize, refine, d_res, s, binned);
@@ -556,7 +560,11 @@ int kt_match_sharded_end_device(kt_ctx *c, int count, const int *d_bbeg, const i
     hipLaunchKernelGGL(kt_exchange_kernel, dim3(count), dim3(KT_THREADS), 0, s, c->g, c->d_state, c->d_resp,
                        c->d_posmax, (long long *)d_exchange, 1);
     KCHK(hipGetLastError());
-    KT_LAUNCH(K_SELECT, kt_select_kernel, dim3(count), dim3(KT_THREADS), 0, s, c->g, c->d_state, c->d_resp,
+    if (c->g.nxy * c->g.nxy > 512)
+        KT_LAUNCH(K_SELECT, kt_select_kernel<1024>, dim3(count), dim3(1024), 0, s, c->g, c->d_state, c->d_resp,
+              c->d_posmax, c->d_tie_idx, c->d_tie_val, 0, do_refine ? 1 : 0, d_res);
+    else
+        KT_LAUNCH(K_SELECT, kt_select_kernel<KT_THREADS>, dim3(count), dim3(KT_THREADS), 0, s, c->g, c->d_state, c->d_resp,
               c->d_posmax, c->d_tie_idx, c->d_tie_val, 0, do_refine ? 1 : 0, d_res);
     return kt_chunk_finish(c, count, d_bbeg, d_bidx, do_penalize ? 1 : 0, do_refine ? 1 : 0, d_res, s,
                            c->sharded_binned);

@@ -1197,12 +1197,15 @@ kt_exchange_kernel(KtGeom g, KtState *st, double *resp, unsigned long long *posm
 
 // =================================================================================================
 // kt_select_kernel: best, tie average, positional covariance, response expansion
+// (KT_SEL_THREADS = 1024 for large windows: the loop window's 101 x 101 positions take 10 block rounds
+// instead of 40; 256 for the sequential matcher's 16 x 16, where the wider block measured slower)
 // =================================================================================================
-__global__ void __launch_bounds__(KT_THREADS)
+template <int KT_SEL_THREADS>
+__global__ void __launch_bounds__(KT_SEL_THREADS)
 kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigned long long *posmax, int *tie_idx,
                  double4 *tie_val, int pass, int refine, kt_result *out)
 {
-    __shared__ int sw[4];
+    __shared__ int sw[KT_SEL_THREADS / 64];
     __shared__ int s_n;
     __shared__ double s_mean[3];
     __shared__ int s_err;
@@ -1232,7 +1235,7 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
     // (coalesced across the threads); ordering the ties by thread within a round keeps pose order.
     const int npos = nxy * nxy;
     unsigned long long *pmw = posmax + (size_t)m * npos;
-    for (int base = 0; base < npos; base += KT_THREADS) {
+    for (int base = 0; base < npos; base += KT_SEL_THREADS) {
         const int pos = base + tid;
         int c = 0;
         double mx = 0.0;
@@ -1250,7 +1253,7 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
             }
         if (pos < npos) pmw[pos] = kt_bits(mx);
         int tot;
-        int pre = kt_block_exscan(c, sw, &tot);
+        int pre = kt_block_exscan_n<KT_SEL_THREADS / 64>(c, sw, &tot);
         const int n0 = s_n;
         if (c)
             for (int a = 0; a < nA; ++a)
@@ -1260,7 +1263,7 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
         __syncthreads();
     }
     const int nt = s_n;
-    for (int t = tid; t < nt; t += KT_THREADS) {
+    for (int t = tid; t < nt; t += KT_SEL_THREADS) {
         const int i = ti[t];
         const int a = i % nA, pos = i / nA;
         const int ix = pos % nxy, iy = pos / nxy;
@@ -1308,7 +1311,7 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
         __syncthreads();
         const int npos = nxy * nxy;
         // probability-grid cell of every coarse column / row (WorldToGrid of the pose positions)
-        for (int i = tid; i < nxy; i += KT_THREADS) {
+        for (int i = tid; i < nxy; i += KT_SEL_THREADS) {
             const double v = startX + (double)(uint32_t)i * g.cres;
             const int pgx = kt_w2g(cx + v, pgox, g.scale), pgy = kt_w2g(cy + v, pgoy, g.scale);
             s_pcx[i] = pgx;
@@ -1317,7 +1320,7 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
                 s_err = 2;  // "Index out of range in probability search" (Mapper.cpp:446)
         }
         __syncthreads();
-        for (int base = 0; base < npos; base += KT_THREADS) {
+        for (int base = 0; base < npos; base += KT_SEL_THREADS) {
             const int i = base + tid;
             int f = 0;
             double val = 0.0;
@@ -1340,7 +1343,7 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
                 f = val >= lo ? 1 : 0;
             }
             int tot;
-            const int pre = kt_block_exscan(f, sw, &tot);
+            const int pre = kt_block_exscan_n<KT_SEL_THREADS / 64>(f, sw, &tot);
             const int n0 = s_n;
             if (f) {
                 const int ix = i % nxy, iy = i / nxy;
@@ -1404,7 +1407,7 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
     __syncthreads();
     if (S.pass == pass + 1) {
         unsigned long long *pm = posmax + (size_t)m * nxy * nxy;
-        for (int i = tid; i < nxy * nxy; i += KT_THREADS) pm[i] = 0ull;
+        for (int i = tid; i < nxy * nxy; i += KT_SEL_THREADS) pm[i] = 0ull;
     }
 }
 

@@ -119,7 +119,18 @@ int kt_geometry(const kt_laser &L, const kt_params &p, KtGeom &g, std::vector<un
     g.coff = 0.5 * ((double)g.side - 1) * g.res;
     g.cres = 2 * g.res;
     g.nxy = (int)(uint32_t)(h_round(g.coff * 2.0 / g.cres) + 1);
-    g.tiles = (g.nxy + KT_TILE - 1) / KT_TILE;
+    {
+        // coarse tile shape: 16 x 16 positions.  SLAM2D_KT_TW = 32 / 64 makes it 32 x 8 / 64 x 4 (a wave's
+        // gather then touches 8 / 4 grid rows of 64 / 128 bytes instead of 16 rows of 32 bytes): measured
+        // slower (loop window 22.3 k -> 20.1 k / 20.8 k matches/s, sequential batch 321 k -> 269 k), so the
+        // coarse kernel is not bound by L2 line requests per gather instruction
+        int tw = 16;
+        if (const char *e = getenv("SLAM2D_KT_TW")) tw = atoi(e);
+        g.clw = tw >= 64 ? 4 : (tw >= 32 ? 3 : 2);
+        tw = 4 << g.clw;
+        g.ctx = (g.nxy + tw - 1) / tw;
+        g.cty = (g.nxy + (256 / tw) - 1) / (256 / tw);
+    }
     if (g.nxy > KT_MAX_NXY) return kfail(KT_EINVAL, "coarse search wider than 1024 positions");
     g.use_expansion = p.use_response_expansion ? 1 : 0;
     g.npass = g.use_expansion ? 4 : 1;
@@ -227,7 +238,7 @@ int kt_chunk_coarse(kt_ctx *c, int count, int pass, int penalize, int shard, int
     const KtGeom &g = c->g;
     // angles per workgroup: 1 (r02 A/B, loop window / sequential batch: 7 angles 5 % / 3 angles 5 % slower,
     // 21 angles 29 % slower -- fewer workgroups left in flight for the gathers); SLAM2D_KT_AG overrides
-    const long long per_angle = (long long)((count + 7) / 8) * 8 * g.tiles * g.tiles;
+    const long long per_angle = (long long)((count + 7) / 8) * 8 * g.ctx * g.cty;
     const int nA = g.nang[pass];
     long long ag = 1;
     if (const char *e = getenv("SLAM2D_KT_AG")) ag = atoll(e);

@@ -42,7 +42,6 @@ namespace s2d {
 
 constexpr int KT_THREADS = 256;
 constexpr int KT_MAX_READINGS = 4096;
-constexpr int KT_TILE = 16;
 constexpr int KT_FINE_MAX_ANG = 64;
 constexpr int KT_MAX_NXY = 1024;  // coarse positions per axis
 constexpr int KT_SEL_ITEMS = 16;
@@ -60,7 +59,8 @@ struct KtGeom {
     int grid_size, border, width, height, ws, data_size;
     int side, probs_ws, half, ksize;
     int n;                             // readings per scan
-    int nxy, tiles;                    // coarse positions per axis, 16-position tiles per axis
+    int nxy;                           // coarse positions per axis
+    int ctx, cty, clw;                 // coarse position tiles along x / y; log2 of gather lanes per tile row
     int npass;                         // 1, or 4 with response expansion
     int nang[4];
     double aoff[4];                    // coarse angle offset per pass
@@ -954,7 +954,7 @@ kt_clear_tiles_kernel(KtGeom g, unsigned char *grids, const int *__restrict__ di
 }
 
 // =================================================================================================
-// kt_coarse_kernel: GetResponse over a 16x16 tile of positions for a group of `ag` consecutive angles
+// kt_coarse_kernel: GetResponse over a tile of 256 positions for a group of `ag` consecutive angles
 //
 // The workgroup keeps its positions and walks its angles: per angle the query's offsets
 // (GridIndexLookup::ComputeOffsets) into LDS, the gathers, the responses.  A position's `ag` responses
@@ -977,7 +977,7 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
 
     const int nA = g.nang[pass];
     const int ngrp = (nA + ag - 1) / ag;
-    const int T2 = g.tiles * g.tiles;
+    const int T2 = g.ctx * g.cty;
     const int W = ngrp * T2;
     // XCD-aware: all work of one match runs on one XCD (blocks are dealt round-robin to the 8 XCDs)
     const int b = blockIdx.x;
@@ -989,7 +989,9 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
     if (S.pass != pass) return;
     const int agrp = w / T2, t = w - agrp * T2;
     const int a0 = agrp * ag, a1 = min(a0 + ag, nA);
-    const int ty = t / g.tiles, tx = t - ty * g.tiles;
+    const int ty = t / g.ctx, tx = t - ty * g.ctx;
+    // tile of 256 positions, TW = 4 << clw wide and TH = 64 >> clw high: a lane gathers 4 positions of a
+    // row (8 bytes), 1 << clw lanes per row
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
     const double cxs = S.center[0], cys = S.center[1], chs = S.center[2];
@@ -1000,8 +1002,9 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
     const double2 *loc = P.loc + (size_t)q * g.n;
     const unsigned char *bad = P.bad + (size_t)q * g.n;
     // this lane's 4 gather positions: row iy, columns ix0 .. ix0 + 3
-    const int iy = ty * KT_TILE + (lane >> 2);
-    const int ix0 = tx * KT_TILE + (lane & 3) * 4;
+    const int clw = g.clw, lmask = (1 << clw) - 1;
+    const int iy = ty * (64 >> clw) + (lane >> clw);
+    const int ix0 = tx * (4 << clw) + (lane & lmask) * 4;
     const double startX = -g.coff;
     int gpos[4];
     bool fast = true;
@@ -1026,8 +1029,8 @@ kt_coarse_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restric
     }
     // the position this thread finalises (one per thread of the tile)
     const int pl = tid >> 2, pj = tid & 3;
-    const int piy = ty * KT_TILE + (pl >> 2);
-    const int pix = tx * KT_TILE + (pl & 3) * 4 + pj;
+    const int piy = ty * (64 >> clw) + (pl >> clw);
+    const int pix = tx * (4 << clw) + (pl & lmask) * 4 + pj;
     const bool pin = piy < g.nxy && pix < g.nxy;
     const size_t pos = (size_t)piy * g.nxy + pix;
     // responses angle-major (resp[a * npos + pos]): a workgroup's 256 positions are one contiguous 2 KB run

@@ -17,6 +17,8 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   nosetup    WRONG RESULTS  hs_update_kernel keeps the fan-group culling of every tile, skips every ray
   noraster   WRONG RESULTS  hs_update_kernel skips the raster loop (tile loop skeleton: clear, barriers)
   ktnorender WRONG RESULTS  kt_addscans_kernel clears, loads and stores its tiles but renders no item
+  lds6       same results   hs_update_kernel with 2.5 KB of unused LDS (7 -> 6 workgroups per CU: occupancy price)
+  lds5       same results   hs_update_kernel with 10 KB of unused LDS (5 workgroups per CU)
   ktnoswar   WRONG RESULTS  kt_addscans_kernel dword render writes the kernel bytes without the byte max
 """
 import os
@@ -47,6 +49,10 @@ PATCHES = {
                  "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n                continue;\n")],
     "noraster": [(K, "                const int4 gb = gbox[b0 >> 6];\n", "                if (b0 >= 0) break;\n                const int4 gb = gbox[b0 >> 6];\n")],
     "ktnorender": [("karto_kernels.hip", "kt_render_items_dw(tileb, sitem, c0, c1,", "kt_render_items_dw(tileb, sitem, c0, c0,")],
+    "lds6": [("hector_capi.hip", "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));\n    const bool single",
+              "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points)) + 2560;\n    const bool single")],
+    "lds5": [("hector_capi.hip", "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));\n    const bool single",
+              "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points)) + 10240;\n    const bool single")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

@@ -798,6 +798,13 @@ def main():
                     "traffic_source": (f"{pmc['source']} (FETCH_SIZE x2 + WRITE_SIZE)" if pmc else None),
                     "traffic_GBps": (round(pmc["traffic_bytes_per_launch"] / avg_s / 1e9, 2) if pmc else None),
                     "min_traffic_per_launch": (int(ctr_i["touched"] * 12 / nlaunch) if dom == "update" else None),
+                    "min_traffic_frac": (round(ctr_i["touched"] * 12 / nlaunch / avg_s / 1e9 / HBM_PEAK_GBS, 5)
+                                         if dom == "update" else None),
+                    "frac_note": ("achieved counts 16 B per cell touch of the reference's raycast (SURVEY 8d), "
+                                  "re-touches of a cell by later beams included; the kernel merges them in LDS, "
+                                  "so achieved can pass the HBM peak: traffic_GBps is the counted HBM rate, "
+                                  "min_traffic_frac the 12 B-per-distinct-cell floor's rate vs peak")
+                    if dom == "update" else None,
                     "avg_launch_ms": round(ms / nlaunch, 5),
                     "timing": "kernel durations from an instrumented pass of K further steps (HIP events "
                               "around each kernel); the headline pass runs without events",

@@ -214,6 +214,20 @@ void end_timed(hs_ctx *c, hipStream_t s)
     hipEventRecord(c->ev_used.back().b, s);
 }
 
+// hs_update_kernel instance: rays in registers for scans of at most UPD_RREG * 256 points (no LDS ray
+// array), else in LDS; SLAM2D_UPD_RAYS_LDS=1 forces the LDS instance (A/B)
+bool upd_rays_in_regs(const hs_ctx *c)
+{
+    static const bool force_lds = getenv("SLAM2D_UPD_RAYS_LDS") && atoi(getenv("SLAM2D_UPD_RAYS_LDS")) != 0;
+    return !force_lds && c->max_points <= UPD_RREG * UPD_THREADS;
+}
+
+size_t upd_shmem_bytes(const hs_ctx *c)
+{
+    const size_t rays = upd_rays_in_regs(c) ? 0 : (size_t)((c->max_points + 3) & ~3);
+    return sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + rays + UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));
+}
+
 int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int xy_stride, const int *n,
                 const float2 *origo, const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s,
                 hipEvent_t wait_before_update = nullptr, const MatchIngest *mi = nullptr)
@@ -223,8 +237,7 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     WorkItem *items = c->d_items + (size_t)part * c->item_cap;
     WorkItem *wholes = c->d_wholes + (size_t)part * c->B * c->levels;
     // the single-kernel update consumes the match kernel's list of updating streams (one part only)
-    const size_t upd_shmem = sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + (size_t)((c->max_points + 3) & ~3) +
-                                                 UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));
+    const size_t upd_shmem = upd_shmem_bytes(c);
     const bool single = c->update_single && upd_shmem <= 65536;
     const bool use_list = single && !c->upd_parts_fixed && mode != MODE_MATCH_ONLY;
     UpdList *wl_cur = use_list ? c->wl[part][c->wl_parity[part]] : nullptr;
@@ -250,8 +263,12 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         UpdList *wl_next = c->wl[part][c->wl_parity[part] ^ 1];
         c->wl_parity[part] ^= 1;
         begin_timed(c, 2, s);
-        hipLaunchKernelGGL(hs_update_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
-                           c->d_state, xy, xy_stride, begin, count, c->max_points, wl_cur, wl_next, c->ncu);
+        if (upd_rays_in_regs(c))
+            hipLaunchKernelGGL((hs_update_kernel<UPD_RREG>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
+                               c->d_state, xy, xy_stride, begin, count, c->max_points, wl_cur, wl_next, c->ncu);
+        else
+            hipLaunchKernelGGL((hs_update_kernel<0>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
+                               c->d_state, xy, xy_stride, begin, count, c->max_points, wl_cur, wl_next, c->ncu);
         end_timed(c, s);
         HCHK(hipGetLastError());
         return HS_OK;
@@ -274,9 +291,14 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         begin_timed(c, 2, s);
         int blocks = 0;
         for (int l = 0; l < c->levels; ++l) blocks += gg.upd_parts[l] * count;
-        hipLaunchKernelGGL(hs_update_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
-                           c->d_state, xy, xy_stride, begin, count, c->max_points, (const UpdList *)nullptr,
-                           (UpdList *)nullptr, c->ncu);
+        if (upd_rays_in_regs(c))
+            hipLaunchKernelGGL((hs_update_kernel<UPD_RREG>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
+                               c->d_state, xy, xy_stride, begin, count, c->max_points, (const UpdList *)nullptr,
+                               (UpdList *)nullptr, c->ncu);
+        else
+            hipLaunchKernelGGL((hs_update_kernel<0>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
+                               c->d_state, xy, xy_stride, begin, count, c->max_points, (const UpdList *)nullptr,
+                               (UpdList *)nullptr, c->ncu);
         end_timed(c, s);
         HCHK(hipGetLastError());
         return HS_OK;
@@ -331,8 +353,7 @@ int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride
 // The pipelined run (hs_run_ranges_device) needs the list-driven single update kernel on every part.
 bool pipeline_ok(const hs_ctx *c)
 {
-    const size_t upd_shmem = sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + (size_t)((c->max_points + 3) & ~3) +
-                                                 UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));
+    const size_t upd_shmem = upd_shmem_bytes(c);
     return c->pipeline && c->update_single && upd_shmem <= 65536 && !c->upd_parts_fixed && c->B >= 2;
 }
 

@@ -1437,6 +1437,13 @@ constexpr int UPD_GROUP_WORDS = 4;  // LDS words per fan group: its bounding box
 
 // Grid: for level l, upd_parts[l] x count blocks (level-major, then part, then stream); part p of a
 // level draws the tiles t = p, p + parts, ... of the scan's tile box (t row-major over the box).
+// RREG > 0: scans of at most RREG * 256 points keep each lane's packed rays (one per fan group it
+// rasters) in registers instead of an LDS array of max_points words -- 4.3 KB less LDS per workgroup
+// at 1081 beams, 8 instead of 7 workgroups per CU (the kernel's VGPRs allow 8).  RREG = 0: rays in LDS.
+// The rays are five named registers picked by selects on the wave-uniform fan-group index (an array
+// or a struct indexed by it ends up in scratch).
+constexpr int UPD_RREG = 5;
+template <int RREG>
 __global__ void __launch_bounds__(UPD_THREADS, S2D_UPD_MINB)
 hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restrict__ state,
                  const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points,
@@ -1449,8 +1456,11 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     // space -- flat accesses with a vmcnt(0) wait that drains the loads the pipeline keeps in flight);
     // lds_barrier's memory clobber orders the accesses
     __shared__ unsigned s_any[2];
-    unsigned *rays = smem + UPD_FIXED_WORDS;               // max_points packed end cells
-    int4 *gbox = reinterpret_cast<int4 *>(rays + ((max_points + 3) & ~3));  // per fan group: x0 y0 x1 y1
+    unsigned *rays = smem + UPD_FIXED_WORDS;               // max_points packed end cells (RREG == 0)
+    int4 *gbox = reinterpret_cast<int4 *>(rays + (RREG > 0 ? 0 : ((max_points + 3) & ~3)));  // per fan group: x0 y0 x1 y1
+    static_assert(RREG == 0 || RREG == UPD_RREG, "RayRegs holds UPD_RREG rays");
+    // RREG > 0: this lane's ray of fan group k = b0 / 256
+    unsigned rr0 = RAY_INVALID, rr1 = RAY_INVALID, rr2 = RAY_INVALID, rr3 = RAY_INVALID, rr4 = RAY_INVALID;
     const int lane = threadIdx.x & 63;
     __shared__ int s_bbox[4];
 
@@ -1496,7 +1506,15 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         unsigned r = RAY_INVALID;
         if (b < n) {
             r = make_ray(g, fr, pts[b]);
-            rays[b] = r;
+            if constexpr (RREG == 0) rays[b] = r;
+        }
+        if constexpr (RREG > 0) {
+            const int k = b0 >> 8;
+            rr0 = k == 0 ? r : rr0;
+            rr1 = k == 1 ? r : rr1;
+            rr2 = k == 2 ? r : rr2;
+            rr3 = k == 3 ? r : rr3;
+            rr4 = k == 4 ? r : rr4;
         }
         int gx0 = x0, gy0 = y0, gx1 = x0, gy1 = y0;  // fan group box: origin + valid ends
         if (r != RAY_INVALID) {
@@ -1576,7 +1594,12 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
                 if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
                 const int b = fan_beam(b0, lane);
-                const unsigned r = b < n ? rays[b] : RAY_INVALID;
+                unsigned r;
+                if constexpr (RREG > 0) {
+                    const int k = b0 >> 8;
+                    r = k == 0 ? rr0 : (k == 1 ? rr1 : (k == 2 ? rr2 : (k == 3 ? rr3 : rr4)));
+                }
+                else r = b < n ? rays[b] : RAY_INVALID;
                 if (r == RAY_INVALID) continue;
                 const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
                 if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;

@@ -77,10 +77,14 @@ def pmc_traffic(kernel: str, cfg_name: str, streams: int):
             d = json.load(f)
     except (OSError, ValueError):
         return None
+    # a template kernel is summarised under its instance name (hs_update_kernel<5>); the latest
+    # summary of this workload (entries are appended in summary order) wins
+    found = None
     for e in d.get("entries", []):
-        if e.get("kernel") == kernel and e.get("config") == cfg_name and e.get("streams") == streams:
-            return e
-    return None
+        k = e.get("kernel", "")
+        if (k == kernel or k.startswith(kernel + "<")) and e.get("config") == cfg_name and e.get("streams") == streams:
+            found = e
+    return found
 
 
 def aggregate_over_ranks(elapsed: float, units: float, device):

@@ -202,17 +202,25 @@ def pose_check(cfg, S, gpu_poses, streams, thresholds=(-1.0, -1.0)):
     import oracle as O
 
     n_scans = gpu_poses.shape[0]
-    e, egt = [], []
+    e, egt, etree = [], [], []
     for i, s in enumerate(streams):
+        # the reference's sequential summation order (the metric), and the kernel's own tree order
+        # (reduce_threads = 256: the oracle the parity tests hold the kernels to bit for bit)
         r = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0)
-        r.set_update_factors(0.4, 0.9)
-        r.set_thresholds(*thresholds)
+        rt = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=256)
+        for h in (r, rt):
+            h.set_update_factors(0.4, 0.9)
+            h.set_thresholds(*thresholds)
         for k in range(n_scans):
-            rp, _, _ = r.process(S.points[s, k, : S.counts[s, k]])
+            pts = S.points[s, k, : S.counts[s, k]]
+            rp, _, _ = r.process(pts)
+            tp, _, _ = rt.process(pts)
             e.append(gpu_poses[k, i].astype(np.float64) - rp.astype(np.float64))
+            etree.append(gpu_poses[k, i].astype(np.float64) - tp.astype(np.float64))
             egt.append(gpu_poses[k, i].astype(np.float64) - S.gt[s, k])
         r.close()
-    e, egt = np.asarray(e), np.asarray(egt)
+        rt.close()
+    e, egt, etree = np.asarray(e), np.asarray(egt), np.asarray(etree)
     egt[:, 2] = np.arctan2(np.sin(egt[:, 2]), np.cos(egt[:, 2]))
     # per logged pose: inside the north-star tolerance?  (float sums in the kernel's tree order vs the
     # reference's sequential order differ in the last bits; a pose that moves an end cell across a cell
@@ -231,6 +239,8 @@ def pose_check(cfg, S, gpu_poses, streams, thresholds=(-1.0, -1.0)):
             "max_abs_xy_m": float(np.abs(e[:, :2]).max()), "max_abs_theta_rad": float(np.abs(e[:, 2]).max()),
             "tolerance": "1e-4 m / 1e-4 rad (north_star)",
             "within_tolerance_frac": float(ok.mean()), "first_outside_tolerance": first,
+            "vs_oracle_tree_order_max_abs": float(np.abs(etree).max()),
+            "vs_oracle_tree_order_exact_frac": float((np.abs(etree).max(axis=1) == 0.0).mean()),
             "vs_ground_truth_rmse_xy_m": float(np.sqrt(np.mean(egt[:, 0] ** 2 + egt[:, 1] ** 2))),
             "vs_ground_truth_rmse_theta_rad": float(np.sqrt(np.mean(egt[:, 2] ** 2)))}
 

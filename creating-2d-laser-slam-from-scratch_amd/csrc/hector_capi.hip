@@ -283,6 +283,7 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
             const int target = count <= 32 ? 2 : 4;
             int p0 = (target * c->ncu + count - 1) / count;
             if (p0 < 2) p0 = 2;
+            if (c->levels == 1 && p0 < 8) p0 = 8;  // as upd_split: a single level fills the grid's tail alone
             for (int l = 0; l < c->levels; ++l) {
                 const int v = p0 >> l;
                 gg.upd_parts[l] = v < 1 ? 1 : (v > 64 ? 64 : v);

@@ -114,13 +114,16 @@ struct UpdList {
 };
 
 // Workgroups per (stream, level) of hs_update_kernel for U updating streams on ncu CUs: about 4 level-0
-// workgroups per CU for small batches (2 for U <= 32), at least 2 for level 0, halved per level
+// workgroups per CU for small batches (2 for U <= 32), at least 2 for level 0 (8 for a single-level
+// map, which has no coarser levels to fill the tail of the grid: c2, 1024 streams, 2 / 3 / 4 / 6 / 8 /
+// 12 / 16 parts = 1.48 / 1.50 / 1.53 / 1.57 / 1.61 / 1.58 / 1.51 M scans/s), halved per level
 // (measured).
 inline __host__ __device__ void upd_split(int U, int ncu, int levels, int *parts, const int *minp)
 {
     const int target = U <= 32 ? 2 : 4;
     int p0 = U > 0 ? (target * ncu + U - 1) / U : 1;
     if (p0 < 2) p0 = 2;
+    if (levels == 1 && p0 < 8) p0 = 8;
     for (int l = 0; l < levels; ++l) {
         int v = p0 >> l;
         if (v < minp[l]) v = minp[l];

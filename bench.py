@@ -556,7 +556,9 @@ def run_karto(args, world, rank, dev):
     from slam2d import karto
 
     cfg = args.config
-    M = args.matches or (512 if cfg == "karto" else 32)
+    # matches per GPU per step (end-of-round-2 sweep: sequential 512 / 1024 / 2048 -> 321 k / 375 k / 387 k
+    # matches/s, loop window 32 / 64 / 128 -> 22.2 k / 25.0 k / 25.6 k: small batches leave the launches' tails)
+    M = args.matches or (2048 if cfg == "karto" else 128)
     K, W = args.steps, args.warmup
     shard = args.karto_shard
     # replicas: every rank its own matches; sharded: every rank the SAME matches, window split by angle

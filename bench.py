@@ -68,23 +68,33 @@ def kernel_symbol(dom: str, ktimes: dict) -> str:
     return f"hs_{dom}_kernel"
 
 
-def pmc_traffic(kernel: str, cfg_name: str, streams: int):
+def pmc_traffic(kernel: str, workload: dict, live_avg_ns: float | None = None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this exact
     workload (tools/profile_gpu.sh + tools/summarize_profile.py): FETCH_SIZE x 2 (gfx950 tallies
-    128-B read requests at 64 B, MI355X_MICROARCH.md) + WRITE_SIZE, both KB -> bytes."""
+    128-B read requests at 64 B, MI355X_MICROARCH.md) + WRITE_SIZE, both KB -> bytes.
+    workload: config, streams, semantics and reduction order must all match the summary's; a summary
+    whose average launch time is more than 25 % away from this run's (another build of the kernel) is
+    refused too.  Returns (entry or None, reason)."""
     try:
         with open(PMC_SUMMARY) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "no profiles/pmc_traffic.json"
     # a template kernel is summarised under its instance name (hs_update_kernel<5>); the latest
     # summary of this workload (entries are appended in summary order) wins
     found = None
     for e in d.get("entries", []):
         k = e.get("kernel", "")
-        if (k == kernel or k.startswith(kernel + "<")) and e.get("config") == cfg_name and e.get("streams") == streams:
+        if not (k == kernel or k.startswith(kernel + "<")):
+            continue
+        if all(e.get(key) == val for key, val in workload.items()):
             found = e
-    return found
+    if found is None:
+        return None, f"no PMC summary for {kernel} on this workload {workload}"
+    if live_avg_ns and abs(found["avg_ns"] - live_avg_ns) > 0.25 * live_avg_ns:
+        return None, (f"PMC summary {found['source']} timed {found['avg_ns'] / 1e3:.1f} us per launch, this run "
+                      f"{live_avg_ns / 1e3:.1f} us: another build, not attached")
+    return found, found["source"]
 
 
 def aggregate_over_ranks(elapsed: float, units: float, device):
@@ -194,37 +204,41 @@ def cpu_baseline_all_cores(cfg, procs, seconds=6.0, thresholds=(-1.0, -1.0)):
                       "oracle -O3"}
 
 
-def pose_check(cfg, S, gpu_poses, streams, thresholds=(-1.0, -1.0)):
+def pose_check(cfg, S, gpu_poses, streams, thresholds=(-1.0, -1.0), order=0):
     """Pose error of the logged GPU streams (device pose log slot i = stream streams[i], every step incl.
     warmup) vs the CPU oracle in the reference's sequential summation order on the same scans -- the
-    metric's 'pose RMSE vs ref' -- plus the absolute error against the synthetic ground truth."""
+    metric's 'pose RMSE vs ref' -- plus the absolute error against the synthetic ground truth.
+    order: the kernel's Hessian summation order (0 = the reference's, the default: the poses must then
+    equal the oracle's bit for bit; 256 = the opt-in tree, also compared with the oracle in that order)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
 
     n_scans = gpu_poses.shape[0]
     e, egt, etree = [], [], []
     for i, s in enumerate(streams):
-        # the reference's sequential summation order (the metric), and the kernel's own tree order
-        # (reduce_threads = 256: the oracle the parity tests hold the kernels to bit for bit)
         r = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=0)
-        rt = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=256)
+        rt = O.HectorOracle(0.05, cfg["map_size"], (0.5, 0.5), cfg["levels"], reduce_threads=order) if order else None
         for h in (r, rt):
-            h.set_update_factors(0.4, 0.9)
-            h.set_thresholds(*thresholds)
+            if h is not None:
+                h.set_update_factors(0.4, 0.9)
+                h.set_thresholds(*thresholds)
         for k in range(n_scans):
             pts = S.points[s, k, : S.counts[s, k]]
             rp, _, _ = r.process(pts)
-            tp, _, _ = rt.process(pts)
             e.append(gpu_poses[k, i].astype(np.float64) - rp.astype(np.float64))
-            etree.append(gpu_poses[k, i].astype(np.float64) - tp.astype(np.float64))
+            if rt is not None:
+                tp, _, _ = rt.process(pts)
+                etree.append(gpu_poses[k, i].astype(np.float64) - tp.astype(np.float64))
             egt.append(gpu_poses[k, i].astype(np.float64) - S.gt[s, k])
         r.close()
-        rt.close()
-    e, egt, etree = np.asarray(e), np.asarray(egt), np.asarray(etree)
+        if rt is not None:
+            rt.close()
+    e, egt = np.asarray(e), np.asarray(egt)
+    etree = np.asarray(etree) if etree else e
     egt[:, 2] = np.arctan2(np.sin(egt[:, 2]), np.cos(egt[:, 2]))
-    # per logged pose: inside the north-star tolerance?  (float sums in the kernel's tree order vs the
-    # reference's sequential order differ in the last bits; a pose that moves an end cell across a cell
-    # boundary changes the map, and later matches can drift apart from there)
+    # per logged pose: inside the north-star tolerance?  (with the reference order every pose is expected
+    # to be EXACT; the tree order reassociates the float sums, and a pose that moves an end cell across a
+    # cell boundary changes the map, so later matches can drift apart from there)
     ok = (np.abs(e[:, 0]) <= 1e-4) & (np.abs(e[:, 1]) <= 1e-4) & (np.abs(e[:, 2]) <= 1e-4)
     bad = np.flatnonzero(~ok)
     first = None
@@ -239,8 +253,10 @@ def pose_check(cfg, S, gpu_poses, streams, thresholds=(-1.0, -1.0)):
             "max_abs_xy_m": float(np.abs(e[:, :2]).max()), "max_abs_theta_rad": float(np.abs(e[:, 2]).max()),
             "tolerance": "1e-4 m / 1e-4 rad (north_star)",
             "within_tolerance_frac": float(ok.mean()), "first_outside_tolerance": first,
-            "vs_oracle_tree_order_max_abs": float(np.abs(etree).max()),
-            "vs_oracle_tree_order_exact_frac": float((np.abs(etree).max(axis=1) == 0.0).mean()),
+            "kernel_summation_order": "reference sequential (OccGridMapUtil.h:94-126)" if not order else f"tree {order}",
+            "exact_frac_vs_reference_order": float((np.abs(e).max(axis=1) == 0.0).mean()),
+            "vs_oracle_in_kernel_order_max_abs": float(np.abs(etree).max()),
+            "vs_oracle_in_kernel_order_exact_frac": float((np.abs(etree).max(axis=1) == 0.0).mean()),
             "vs_ground_truth_rmse_xy_m": float(np.sqrt(np.mean(egt[:, 0] ** 2 + egt[:, 1] ** 2))),
             "vs_ground_truth_rmse_theta_rad": float(np.sqrt(np.mean(egt[:, 2] ** 2)))}
 
@@ -659,6 +675,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--no-copy-probe", action="store_true", help="skip the copy-bandwidth probe")
+    ap.add_argument("--order", choices=["reference", "tree"], default="reference",
+                    help="hector: Hessian summation order of the matcher (the reference's sequential order, default; "
+                         "or the faster 256-thread tree)")
     ap.add_argument("--semantics", choices=["forced", "reference"], default="forced",
                     help="hector: map update every scan (benchmark mode, SURVEY.md 8d) or the node's thresholds "
                          "0.4 m / 0.9 rad (reference semantics, reported separately)")
@@ -721,6 +740,10 @@ def main():
     ref_sem = args.semantics == "reference"
     thr = (0.4, 0.9) if ref_sem else (-1.0, -1.0)
     fleet.set_thresholds(*thr)           # benchmark mode: update every scan; reference: hector_slam.launch
+    if args.order == "tree":
+        fleet.set_reduction_order(HectorFleet.ORDER_TREE256)
+    order = fleet.reduction_order()
+    workload = {"config": args.config, "streams": B, "semantics": args.semantics, "order": order}
     hs = torch.cuda.current_stream(dev).cuda_stream
     # pose log: every 64th stream and the last one (the top of the update lists and of the HBM range)
     log_streams = sorted(set(range(0, B, 64)) | {B - 1})
@@ -804,33 +827,46 @@ def main():
             ab_i = algorithmic_bytes(ctr_i, cfg["levels"])
             dom = max(KERNELS, key=lambda k: ktimes[k][0])
             ms, nlaunch = ktimes[dom]
-            per_launch_bytes = ab_i[dom] / nlaunch
             avg_s = ms / 1e3 / nlaunch
-            achieved = per_launch_bytes / avg_s / 1e9
             ksym = kernel_symbol(dom, ktimes)
-            pmc = pmc_traffic(ksym, args.config, B)
+            pmc, pmc_why = pmc_traffic(ksym, workload, avg_s * 1e9)
+            # distinct-cell floor of the update: every cell the scan changes is read once (4 B log-odds)
+            # and written once (4 B log-odds + 4 B updateIndex) -- the least any once-per-scan update moves
+            floor = ctr_i["touched"] * 12 / nlaunch if dom == "update" else ab_i[dom] / nlaunch
+            model_8d = ab_i[dom] / nlaunch
+            # achieved / frac: counted HBM bytes (PMC summary of this exact workload) when available, else
+            # the distinct-cell floor -- both are bytes the kernel really moves, so frac <= 1.  SURVEY 8d's
+            # touch model (16 B per cell touch, re-touches by later beams included, which the kernel merges
+            # in LDS) is reported as bytes only.
+            moved = pmc["traffic_bytes_per_launch"] if pmc else floor
+            achieved = moved / avg_s / 1e9
+            mpmc, _ = pmc_traffic("hs_match_kernel", workload, None)
             roof = {"bound": "hbm", "kernel": ksym, "achieved": round(achieved, 2),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
-                    "traffic_source": (f"{pmc['source']} (FETCH_SIZE x2 + WRITE_SIZE)" if pmc else None),
-                    "traffic_GBps": (round(pmc["traffic_bytes_per_launch"] / avg_s / 1e9, 2) if pmc else None),
-                    "min_traffic_per_launch": (int(ctr_i["touched"] * 12 / nlaunch) if dom == "update" else None),
-                    "min_traffic_frac": (round(ctr_i["touched"] * 12 / nlaunch / avg_s / 1e9 / HBM_PEAK_GBS, 5)
-                                         if dom == "update" else None),
-                    "frac_note": ("achieved counts 16 B per cell touch of the reference's raycast (SURVEY 8d), "
-                                  "re-touches of a cell by later beams included; the kernel merges them in LDS, "
-                                  "so achieved can pass the HBM peak: traffic_GBps is the counted HBM rate, "
-                                  "min_traffic_frac the 12 B-per-distinct-cell floor's rate vs peak")
+                    "achieved_basis": ("PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) / avg launch time"
+                                       if pmc else "distinct-cell floor (12 B per distinct cell) / avg launch time"),
+                    "traffic_source": (f"{pmc_why} (FETCH_SIZE x2 + WRITE_SIZE)" if pmc else pmc_why),
+                    "min_traffic_per_launch": int(floor) if dom == "update" else None,
+                    "min_traffic_frac": (round(floor / avg_s / 1e9 / HBM_PEAK_GBS, 5) if dom == "update" else None),
+                    "traffic_over_floor": (round(pmc["traffic_bytes_per_launch"] / floor, 3) if pmc and dom == "update"
+                                           else None),
+                    "survey_8d_bytes_per_launch": int(model_8d),
+                    "survey_8d_note": ("SURVEY 8d: 16 B per cell touch of the reference's raycast (8 B LogOddsCell read "
+                                       "+ write), re-touches of a cell by later beams included; the kernel merges them "
+                                       "in LDS and moves each distinct cell once, so this is work, not traffic")
                     if dom == "update" else None,
                     "avg_launch_ms": round(ms / nlaunch, 5),
                     "timing": "kernel durations from an instrumented pass of K further steps (HIP events "
                               "around each kernel); the headline pass runs without events",
                     "instrumented_ms_per_step": round(elapsed_i / P * 1e3, 4),
-                    "alg_bytes_per_launch": int(per_launch_bytes),
                     "kernel_ms_per_step": {k: round(ktimes[k][0] / max(ktimes[k][1], 1), 5) for k in KERNELS},
-                    "whole_step_GBps": round(ab["total"] / K / (t_max / K) / 1e9, 2),
-                    "whole_step_frac": round(ab["total"] / t_max / 1e9 / HBM_PEAK_GBS, 5),
+                    # the north star's "HBM-read roofline": SURVEY 8d's read subset (match gathers + 8 B per cell
+                    # touch) over the step's wall time, and the counted reads of the step's kernels (PMC)
                     "read_only_frac": round(ab["read_only"] / t_max / 1e9 / HBM_PEAK_GBS, 5),
+                    "read_only_frac_counters": (round((2 * pmc["fetch_kb"] + 2 * mpmc["fetch_kb"]) * 1024 * K
+                                                      / t_max / 1e9 / HBM_PEAK_GBS, 5)
+                                                if (pmc and mpmc and dom == "update") else None),
                     "alg_bytes_per_scan": int(ab["total"] / max(B * K, 1)),
                     "cells_per_scan": round(ctr["cells"] / max(B * K, 1), 1),
                     "distinct_cells_per_scan": round(ctr["touched"] / max(B * K, 1), 1)}
@@ -841,7 +877,7 @@ def main():
             cpu = cpu_baseline(cfg, thresholds=thr)
             if args.cpu_cores > 1:
                 cpu["all_cores"] = cpu_baseline_all_cores(cfg, args.cpu_cores, thresholds=thr)
-        pose = pose_check(cfg, S, d_plog.cpu().numpy(), log_streams, thresholds=thr)
+        pose = pose_check(cfg, S, d_plog.cpu().numpy(), log_streams, thresholds=thr, order=order)
         out = {"metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K,
                "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
@@ -857,7 +893,8 @@ def main():
                                      + (", two fleet halves pipelined (SLAM2D_PIPELINE=1)"
                                         if os.environ.get("SLAM2D_PIPELINE", "0") not in ("", "0") else ""))
                                     if pipelined else "one batch call per step"),
-                          "parallelism": f"replicas x{world}",
+                          "parallelism": f"replicas x{world}", "semantics": args.semantics,
+                          "reduction_order": order,
                           "map_updates_per_scan": round(ctr["updates"] / max(B * K, 1), 4)},
                "roofline": roof, "cpu_baseline": cpu, "pose_vs_ref": pose}
         if cpu:

@@ -82,6 +82,9 @@ struct hs_ctx {
     // batch split into parts on separate HIP streams so one part's tile kernel overlaps another
     // part's match / bin kernels (they are latency-bound at low occupancy)
     int nparts = 1;
+    // queue slots (work queue, segment / item / whole ranges) = parts that can be in flight: nparts, and at
+    // least 2 when the pipelined run (SLAM2D_PIPELINE=1) drives the two fleet halves as parts 0 and 1
+    int nq = 1;
     int update_single = 1;  // hs_update_kernel (per stream-level, default) or bin + tile kernels
     int ncu = 256;
     bool upd_parts_fixed = false;  // SLAM2D_UPD_PARTS given: no batch-size adaptive split
@@ -97,6 +100,9 @@ struct hs_ctx {
     // kernel already fills the CUs, and a concurrent match slows it more than it hides), so off by default.
     bool pipeline = false;
     bool fuse_ingest = true;  // range arrays: ingest inside the match kernel (SLAM2D_FUSE_INGEST=0: own kernel)
+    // Hessian summation order of hs_match_kernel: 0 = the reference's sequential point order (default),
+    // 256 = the 256-thread tree (hs_set_reduction_order / SLAM2D_MATCH_ORDER=tree)
+    int reduce_order = 0;
     hipEvent_t ev_upd[MAX_PARTS] = {};
     // the last device work of the context (every *_device call waits for it on its own stream, so the
     // per-context scratch -- update lists, ingest buffers, queues -- is never used by two streams at once)
@@ -104,10 +110,13 @@ struct hs_ctx {
     // serialises host calls on one context (e.g. a publish thread's hs_get_map against the spin
     // thread's hs_update, hector_slam.cc:277 vs :201)
     std::recursive_mutex mu;
-    // scan ingest (hs_set_laser): unit vectors, geometry, the batch's DataContainers
+    // scan ingest (hs_set_laser): unit vectors, geometry
     bool has_laser = false;
     IngestGeom ingest{};
     double2 *d_cs = nullptr;
+    // per-stream DataContainer buffer [B][max_points]: the range-array entry points ingest into it, and
+    // after every match it holds the stream's matched container, which MapRepMultiMap keeps for the
+    // update of levels >= 1 (StreamState::mc_n / mc_origo; MapRepMultiMap.h:161, :187)
     float2 *d_ixy = nullptr;
     int *d_in = nullptr;
     float2 *d_iorigo = nullptr;
@@ -177,12 +186,30 @@ StreamState initial_state()
     return st;
 }
 
-int reset_all(hs_ctx *c)
+// full (hs_create): every stream from the constructor state.  Otherwise HectorSlamProcessor::reset
+// (HectorSlamProcessor.h:111-117): lastMapUpdatePose = FLT_MAX, lastScanMatchPose = 0, every grid
+// cleared (GridMapBase::reset -> clear, GridMapBase.h:94-113); what the reference keeps is kept: the
+// grids' currUpdateIndex / lastUpdateIndex (OccGridMapBase.h:334, GridMapBase.h:413), lastScanMatchCov
+// and MapRepMultiMap's stored containers (MapRepMultiMap.h:102-110 resets the maps only).
+int reset_all(hs_ctx *c, bool full)
 {
     size_t nwords = c->cells_bytes / sizeof(float);
     hipLaunchKernelGGL(hs_fill_cells_kernel, dim3(4096), dim3(256), 0, c->stream, c->d_cells, nwords);
     HCHK(hipGetLastError());
     std::vector<StreamState> h(c->B, initial_state());
+    if (!full) {
+        std::vector<StreamState> old(c->B);
+        HCHK(hipMemcpyAsync(old.data(), c->d_state, sizeof(StreamState) * c->B, hipMemcpyDeviceToHost, c->stream));
+        HCHK(hipStreamSynchronize(c->stream));
+        for (int s = 0; s < c->B; ++s) {
+            StreamState &o = old[s];
+            o.last_upd_pose[0] = o.last_upd_pose[1] = o.last_upd_pose[2] = FLT_MAX;
+            o.pose[0] = o.pose[1] = o.pose[2] = 0.0f;
+            o.do_update = 0;
+            o.step_index = 0;
+            h[s] = o;
+        }
+    }
     HCHK(hipMemcpyAsync(c->d_state, h.data(), sizeof(StreamState) * c->B, hipMemcpyHostToDevice, c->stream));
     for (int p = 0; p < MAX_PARTS; ++p)
         for (int i = 0; i < 2; ++i)
@@ -232,19 +259,26 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
                 const float2 *origo, const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s,
                 hipEvent_t wait_before_update = nullptr, const MatchIngest *mi = nullptr)
 {
+    if (part < 0 || part >= c->nq) return fail(HS_EINVAL, "internal: part without a queue slot");
     WorkQueue *wq = c->d_wq + part;
     uint4 *segs = c->d_segs + (size_t)part * c->seg_cap;
     WorkItem *items = c->d_items + (size_t)part * c->item_cap;
     WorkItem *wholes = c->d_wholes + (size_t)part * c->B * c->levels;
-    // the single-kernel update consumes the match kernel's list of updating streams (one part only)
+    // the single-kernel update consumes the match kernel's list of updating streams (wl[part][parity]: one
+    // pair of lists per part)
     const size_t upd_shmem = upd_shmem_bytes(c);
     const bool single = c->update_single && upd_shmem <= 65536;
     const bool use_list = single && !c->upd_parts_fixed && mode != MODE_MATCH_ONLY;
     UpdList *wl_cur = use_list ? c->wl[part][c->wl_parity[part]] : nullptr;
     begin_timed(c, 0, s);
-    hipLaunchKernelGGL(hs_match_kernel, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state, xy,
-                       xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur, c->ingest,
-                       mi ? *mi : MatchIngest{});
+    if (c->reduce_order == 0)
+        hipLaunchKernelGGL(hs_match_kernel<true>, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state,
+                           xy, xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur, c->ingest,
+                           mi ? *mi : MatchIngest{}, c->d_ixy, c->max_points);
+    else
+        hipLaunchKernelGGL(hs_match_kernel<false>, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state,
+                           xy, xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur, c->ingest,
+                           mi ? *mi : MatchIngest{}, c->d_ixy, c->max_points);
     end_timed(c, s);
     HCHK(hipGetLastError());
     if (mode == MODE_MATCH_ONLY) return HS_OK;
@@ -265,10 +299,12 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         begin_timed(c, 2, s);
         if (upd_rays_in_regs(c))
             hipLaunchKernelGGL((hs_update_kernel<UPD_RREG>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
-                               c->d_state, xy, xy_stride, begin, count, c->max_points, wl_cur, wl_next, c->ncu);
+                               c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, wl_cur,
+                               wl_next, c->ncu);
         else
             hipLaunchKernelGGL((hs_update_kernel<0>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
-                               c->d_state, xy, xy_stride, begin, count, c->max_points, wl_cur, wl_next, c->ncu);
+                               c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, wl_cur,
+                               wl_next, c->ncu);
         end_timed(c, s);
         HCHK(hipGetLastError());
         return HS_OK;
@@ -294,19 +330,19 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         for (int l = 0; l < c->levels; ++l) blocks += gg.upd_parts[l] * count;
         if (upd_rays_in_regs(c))
             hipLaunchKernelGGL((hs_update_kernel<UPD_RREG>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
-                               c->d_state, xy, xy_stride, begin, count, c->max_points, (const UpdList *)nullptr,
+                               c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, (const UpdList *)nullptr,
                                (UpdList *)nullptr, c->ncu);
         else
             hipLaunchKernelGGL((hs_update_kernel<0>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
-                               c->d_state, xy, xy_stride, begin, count, c->max_points, (const UpdList *)nullptr,
+                               c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, (const UpdList *)nullptr,
                                (UpdList *)nullptr, c->ncu);
         end_timed(c, s);
         HCHK(hipGetLastError());
         return HS_OK;
     }
     begin_timed(c, 1, s);
-    hipLaunchKernelGGL(hs_bin_kernel, dim3(count), dim3(BIN_THREADS), 0, s, c->geom, c->d_state, xy, xy_stride, begin,
-                       c->max_points, c->d_rays, segs, items, wholes, wq, c->seg_cap, c->item_cap);
+    hipLaunchKernelGGL(hs_bin_kernel, dim3(count), dim3(BIN_THREADS), 0, s, c->geom, c->d_state, xy, xy_stride, c->d_ixy,
+                       c->max_points, begin, c->max_points, c->d_rays, segs, items, wholes, wq, c->seg_cap, c->item_cap);
     end_timed(c, s);
     HCHK(hipGetLastError());
     begin_timed(c, 2, s);
@@ -355,7 +391,7 @@ int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride
 bool pipeline_ok(const hs_ctx *c)
 {
     const size_t upd_shmem = upd_shmem_bytes(c);
-    return c->pipeline && c->update_single && upd_shmem <= 65536 && !c->upd_parts_fixed && c->B >= 2;
+    return c->pipeline && c->nq >= 2 && c->update_single && upd_shmem <= 65536 && !c->upd_parts_fixed && c->B >= 2;
 }
 
 int check_stream(hs_ctx *c, int stream) { return (c && stream >= 0 && stream < c->B) ? HS_OK : HS_EINVAL; }
@@ -458,7 +494,8 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         (e = hipMalloc(&c->d_hint1, sizeof(float) * 3)) != hipSuccess ||
         (e = hipMalloc(&c->d_out_pose, sizeof(float) * 3 * num_streams)) != hipSuccess ||
         (e = hipMalloc(&c->d_out_cov, sizeof(float) * 9 * num_streams)) != hipSuccess ||
-        (e = hipMalloc(&c->d_occ, (size_t)map_size_x * map_size_y)) != hipSuccess) {
+        (e = hipMalloc(&c->d_occ, (size_t)map_size_x * map_size_y)) != hipSuccess ||
+        (e = hipMalloc(&c->d_ixy, sizeof(float2) * (size_t)num_streams * max_points)) != hipSuccess) {
         hs_destroy(c);
         return fail(HS_ENOMEM, "hipMalloc", e);
     }
@@ -482,6 +519,8 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         c->tile_grid = ncu * (tg ? atoi(tg) : per_cu);
         const char *pp = getenv("SLAM2D_PIPELINE");
         c->pipeline = pp && atoi(pp) != 0;
+        const char *mo = getenv("SLAM2D_MATCH_ORDER");
+        c->reduce_order = (mo && strcmp(mo, "tree") == 0) ? MATCH_THREADS : 0;
         const char *fi = getenv("SLAM2D_FUSE_INGEST");
         c->fuse_ingest = !(fi && atoi(fi) == 0);
         const char *np = getenv("SLAM2D_PARTS");
@@ -516,11 +555,12 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         }
         if (c->nparts < 1) c->nparts = 1;
         if (c->nparts > MAX_PARTS) c->nparts = MAX_PARTS;
+        c->nq = (c->pipeline && c->nparts < 2) ? 2 : c->nparts;
         // per-part capacities (test hooks SLAM2D_SEG_CAP / SLAM2D_ITEM_CAP set them directly)
         if (const char *e2 = getenv("SLAM2D_SEG_CAP")) c->seg_cap = (unsigned)atoll(e2);
-        else c->seg_cap = (unsigned)((size_t)c->seg_cap / c->nparts + (1u << 16));
+        else c->seg_cap = (unsigned)((size_t)c->seg_cap / c->nq + (1u << 16));
         if (const char *e2 = getenv("SLAM2D_ITEM_CAP")) c->item_cap = (unsigned)atoll(e2);
-        else c->item_cap = (unsigned)((size_t)c->item_cap / c->nparts + (1u << 10));
+        else c->item_cap = (unsigned)((size_t)c->item_cap / c->nq + (1u << 10));
         for (int p = 0; p < MAX_PARTS; ++p) {
             if ((e = hipStreamCreateWithFlags(&c->pstream[p], hipStreamDefault)) != hipSuccess ||
                 (e = hipEventCreateWithFlags(&c->ev_done[p], hipEventDisableTiming)) != hipSuccess ||
@@ -536,10 +576,10 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         }
     }
     if ((e = hipMalloc(&c->d_rays, sizeof(unsigned) * (size_t)num_streams * levels * max_points)) != hipSuccess ||
-        (e = hipMalloc(&c->d_segs, sizeof(uint4) * (size_t)c->seg_cap * c->nparts)) != hipSuccess ||
-        (e = hipMalloc(&c->d_items, sizeof(WorkItem) * (size_t)c->item_cap * c->nparts)) != hipSuccess ||
-        (e = hipMalloc(&c->d_wholes, sizeof(WorkItem) * (size_t)num_streams * levels * c->nparts)) != hipSuccess ||
-        (e = hipMalloc(&c->d_wq, sizeof(WorkQueue) * c->nparts)) != hipSuccess) {
+        (e = hipMalloc(&c->d_segs, sizeof(uint4) * (size_t)c->seg_cap * c->nq)) != hipSuccess ||
+        (e = hipMalloc(&c->d_items, sizeof(WorkItem) * (size_t)c->item_cap * c->nq)) != hipSuccess ||
+        (e = hipMalloc(&c->d_wholes, sizeof(WorkItem) * (size_t)num_streams * levels * c->nq)) != hipSuccess ||
+        (e = hipMalloc(&c->d_wq, sizeof(WorkQueue) * c->nq)) != hipSuccess) {
         hs_destroy(c);
         return fail(HS_ENOMEM, "hipMalloc", e);
     }
@@ -554,14 +594,14 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         memset(&q, 0, sizeof(q));
         q.item_cap = c->item_cap;
         q.seg_cap = c->seg_cap;
-        for (int p = 0; p < c->nparts; ++p) {
+        for (int p = 0; p < c->nq; ++p) {
             if ((e = hipMemcpy(c->d_wq + p, &q, sizeof(q), hipMemcpyHostToDevice)) != hipSuccess) {
                 hs_destroy(c);
                 return fail(HS_EHIP, "hipMemcpy(work queue)", e);
             }
         }
     }
-    int rc = reset_all(c);
+    int rc = reset_all(c, true);
     if (rc != HS_OK) {
         hs_destroy(c);
         return rc;
@@ -620,7 +660,7 @@ int hs_reset(hs_ctx *c)
     if (!c) return fail(HS_EINVAL, "ctx is NULL");
     LOCK(c);
     HCHK(hipDeviceSynchronize());
-    return reset_all(c);
+    return reset_all(c, false);
 }
 
 int hs_set_update_factors(hs_ctx *c, float free_factor, float occupied_factor)
@@ -909,7 +949,6 @@ int hs_set_laser(hs_ctx *c, const hs_laser *L, const double *unit_vectors)
     hipError_t e;
     if (!c->d_cs) {
         if ((e = hipMalloc(&c->d_cs, sizeof(double2) * (size_t)c->max_points)) != hipSuccess ||
-            (e = hipMalloc(&c->d_ixy, sizeof(float2) * (size_t)c->B * c->max_points)) != hipSuccess ||
             (e = hipMalloc(&c->d_in, sizeof(int) * (size_t)c->B)) != hipSuccess ||
             (e = hipMalloc(&c->d_iorigo, sizeof(float2) * (size_t)c->B)) != hipSuccess ||
             (e = hipMalloc(&c->d_ranges1, sizeof(float) * (size_t)c->max_points)) != hipSuccess)
@@ -949,8 +988,9 @@ int hs_step_ranges_batch_device(hs_ctx *c, int stream_begin, int count, const fl
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
     int rc = dev_enter(c, s);
     if (rc == HS_OK)
-        rc = launch_ranges_step(c, stream_begin, count, d_ranges, range_stride, c->d_ixy, c->max_points, c->d_in,
-                                c->d_iorigo, d_hints, nullptr, nullptr, s);
+        rc = launch_ranges_step(c, stream_begin, count, d_ranges, range_stride,
+                                c->d_ixy + (size_t)stream_begin * c->max_points, c->max_points, c->d_in, c->d_iorigo,
+                                d_hints, nullptr, nullptr, s);
     return rc == HS_OK ? dev_leave(c, s) : rc;
 }
 
@@ -964,8 +1004,8 @@ int hs_update_ranges(hs_ctx *c, int stream, const float *ranges, float pose_out[
     if (c->ingest.n > 0)
         HCHK(hipMemcpyAsync(c->d_ranges1, ranges, sizeof(float) * c->ingest.n, hipMemcpyHostToDevice, c->stream));
     // scanCallback: startEstimate = getLastScanMatchPose() (hector_slam.cc:201), i.e. no explicit hint
-    int rc = launch_ranges_step(c, stream, 1, c->d_ranges1, c->max_points, c->d_pts1, c->max_points, c->d_n1,
-                                c->d_origo1, nullptr, c->d_out_pose, c->d_out_cov, c->stream);
+    int rc = launch_ranges_step(c, stream, 1, c->d_ranges1, c->max_points, c->d_ixy + (size_t)stream * c->max_points,
+                                c->max_points, c->d_n1, c->d_origo1, nullptr, c->d_out_pose, c->d_out_cov, c->stream);
     if (rc == HS_OK) rc = dev_leave(c, c->stream);
     if (rc != HS_OK) return rc;
     StreamState st;
@@ -1025,10 +1065,10 @@ int hs_get_queue_stats(hs_ctx *c, int64_t out[8], int reset_stamps)
     WorkQueue q[MAX_PARTS];
     unsigned long long st[8];
     HCHK(hipDeviceSynchronize());
-    HCHK(hipMemcpy(q, c->d_wq, sizeof(WorkQueue) * c->nparts, hipMemcpyDeviceToHost));
+    HCHK(hipMemcpy(q, c->d_wq, sizeof(WorkQueue) * c->nq, hipMemcpyDeviceToHost));
     HCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
     for (int k = 0; k < 4; ++k) out[k] = 0;
-    for (int p = 0; p < c->nparts; ++p) {
+    for (int p = 0; p < c->nq; ++p) {
         out[0] += q[p].item_used;
         out[1] += q[p].seg_used;
         out[2] += q[p].whole_used;
@@ -1074,6 +1114,21 @@ int hs_set_pose_log_slots(hs_ctx *c, float *d_buf, const int *d_slot_of_stream, 
 }
 
 void *hs_get_stream(hs_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int hs_set_reduction_order(hs_ctx *c, int order)
+{
+    if (!c || (order != HS_ORDER_REFERENCE && order != HS_ORDER_TREE256)) return fail(HS_EINVAL, "bad reduction order");
+    LOCK(c);
+    c->reduce_order = order;
+    return HS_OK;
+}
+
+int hs_get_reduction_order(hs_ctx *c, int *order_out)
+{
+    if (!c || !order_out) return fail(HS_EINVAL, "NULL argument");
+    *order_out = c->reduce_order;
+    return HS_OK;
+}
 
 int hs_set_timing(hs_ctx *c, int enable)
 {

@@ -85,7 +85,11 @@ struct alignas(16) StreamState {
     unsigned long long tot_steps;     // steps
     unsigned long long tot_touched;   // distinct cells written by the grid update (Σ levels, per scan)
     int step_index;                   // steps since hs_reset (pose-log row)
-    int pad_;
+    // MapRepMultiMap::dataContainers (MapRepMultiMap.h:89, :161): the DataContainer of the last
+    // matchData, which updateByScan draws into levels >= 1 (:187).  Its points (level-0 scale) live in
+    // the context's per-stream container buffer; empty (mc_n = 0) until the first match.
+    int mc_n;
+    float mc_origo[2];
 };
 
 // Binned grid-update work queue (hs_bin_kernel -> hs_tile_kernel).

@@ -251,9 +251,11 @@ __device__ __forceinline__ void point_fetch(const float *__restrict__ lvl_words,
     }
 }
 
+// The 9 per-point terms t = {dTr0, dTr1, dTr2, H00, H11, H22, H01, H02, H12} of one point
+// (OccGridMapUtil.h:106-125: the products the reference adds into dTr / H).
 // probs: pf.l already holds the 4 probabilities (neighbourhood cache) instead of log-odds
 template <bool probs = false>
-__device__ __forceinline__ void point_accum(const PointFetch &pf, float cs, float sn, float *acc)
+__device__ __forceinline__ void point_terms(const PointFetch &pf, float cs, float sn, float *t)
 {
     float v, gx, gy;
     if (!pf.in) {
@@ -280,15 +282,88 @@ __device__ __forceinline__ void point_accum(const PointFetch &pf, float cs, floa
     float fun = 1.0f - v;
     // sinRot/cosRot (:87-88) are the same values as the transform's sn/cs
     float rot = ((-sn * px - cs * py) * gx + (cs * px - sn * py) * gy);
-    acc[0] = acc[0] + gx * fun;
-    acc[1] = acc[1] + gy * fun;
-    acc[2] = acc[2] + rot * fun;
-    acc[3] = acc[3] + gx * gx;
-    acc[4] = acc[4] + gy * gy;
-    acc[5] = acc[5] + rot * rot;
-    acc[6] = acc[6] + gx * gy;
-    acc[7] = acc[7] + gx * rot;
-    acc[8] = acc[8] + gy * rot;
+    t[0] = gx * fun;
+    t[1] = gy * fun;
+    t[2] = rot * fun;
+    t[3] = gx * gx;
+    t[4] = gy * gy;
+    t[5] = rot * rot;
+    t[6] = gx * gy;
+    t[7] = gx * rot;
+    t[8] = gy * rot;
+}
+
+// acc[k] += t[k]: one thread's strided partial sums (the tree order, below)
+template <bool probs = false>
+__device__ __forceinline__ void point_accum(const PointFetch &pf, float cs, float sn, float *acc)
+{
+    float t[9];
+    point_terms<probs>(pf, cs, sn, t);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[k] = acc[k] + t[k];
+}
+
+// ---- the reference's summation order (default) -------------------------------------------------
+// getCompleteHessianDerivs adds the points' terms one after the other in point order
+// (OccGridMapUtil.h:94-126: dTr[k] += ..., H(i, j) += ... for i = 0 .. size-1, in float).  Float
+// addition is not associative, so the only way to get the reference's H / b bit for bit is that same
+// chain of adds.  The points are processed in chunks of 256 (point i = chunk * 256 + thread); a chunk's
+// 9 x 256 terms go to LDS term-major, and 9 lanes of one wave (lane k = term k) extend the 9 running
+// sums over the chunk in point order while the other waves compute the next chunk's terms.
+// Rows are SEQ_STRIDE words: 16-B aligned, and row k starts on bank 4k, so the 9 lanes' 16-B reads
+// hit distinct banks.
+constexpr int SEQ_STRIDE = MATCH_THREADS + 4;
+constexpr int SEQ_WORDS = 9 * SEQ_STRIDE;
+
+// run + T[lane][0] + T[lane][1] + ... + T[lane][cnt - 1], left to right
+__device__ __forceinline__ float seq_chain(const float *T, int lane, int cnt, float run)
+{
+    const float4 *row = reinterpret_cast<const float4 *>(T + lane * SEQ_STRIDE);
+    const int c4 = cnt >> 2;
+    int i = 0;
+    for (; i + 3 < c4; i += 4) {
+        const float4 a = row[i], b = row[i + 1], c = row[i + 2], d = row[i + 3];
+        run = run + a.x; run = run + a.y; run = run + a.z; run = run + a.w;
+        run = run + b.x; run = run + b.y; run = run + b.z; run = run + b.w;
+        run = run + c.x; run = run + c.y; run = run + c.z; run = run + c.w;
+        run = run + d.x; run = run + d.y; run = run + d.z; run = run + d.w;
+    }
+    for (; i < c4; ++i) {
+        const float4 a = row[i];
+        run = run + a.x; run = run + a.y; run = run + a.z; run = run + a.w;
+    }
+    const float *tail = T + lane * SEQ_STRIDE + (c4 << 2);
+    for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];
+    return run;
+}
+
+// Workgroup barrier for LDS hand-offs only (waits for this wave's LDS operations, not for its global
+// memory operations; see hs_update_kernel)
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// One chunk of the sequential sum: store this thread's terms t (if has), hand the chunk to the chain
+// wave cw, which extends run (lane k < 9: term k).  first: no earlier chunk of this step is still
+// being read (the previous step ended with a workgroup barrier after the chain).
+__device__ __forceinline__ void seq_chunk(float *T, const float *t, bool has, bool first, int cnt, int cw, float &run)
+{
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (!first) lds_barrier();  // the chain wave has finished reading the previous chunk
+    if (has) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) T[k * SEQ_STRIDE + tid] = t[k];
+    }
+    lds_barrier();
+    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);
+}
+
+// the 9 sums held by lanes 0..8 of the calling (chain) wave, in every lane of it
+__device__ __forceinline__ void seq_gather(float run, float *s)
+{
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(run), k));
 }
 
 // The 64-lane xor butterfly of the Hessian terms, offsets 32, 16, 8, 4, 2, 1 (the oracle's
@@ -323,47 +398,70 @@ __device__ __forceinline__ void wave_butterfly(float (&acc)[NV])
 #endif
 constexpr int MATCH_BATCH = S2D_MATCH_BATCH;  // points per thread with gathers in flight together
 
-// One Gauss-Newton step, ScanMatcher::estimateTransformationLogLh (H/matcher/ScanMatcher.h:107-139).
-// Every thread ends with the same H, b and estimate (xor-butterfly reductions are symmetric).
+// One Gauss-Newton step, ScanMatcher::estimateTransformationLogLh (H/matcher/ScanMatcher.h:107-139),
+// points read from HBM (scans of more than MATCH_THREADS * MATCH_REG_PTS points).
+// Every thread ends with the same H, b and estimate.  SEQ: the reference's sequential sum (seq_chunk);
+// else the tree order (xor butterflies, symmetric).
+template <bool SEQ>
 __device__ __forceinline__ void gn_step(const float *__restrict__ cells, const LevelGeom &g,
                                         const float2 *__restrict__ pts, int n, float f, float *est, float *H,
-                                        float (*red)[MATCH_WAVES][9], int parity, int *clamps)
+                                        float (*red)[MATCH_WAVES][9], int parity, int *clamps, float *seqT)
 {
     const int tid = threadIdx.x;
     const float cs = sdm_cosf(est[2]);
     const float sn = sdm_sinf(est[2]);
-    float acc[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
-    // per-thread order of the points is i = tid, tid + 256, ... (the oracle's reduce_threads order)
-    for (int i0 = tid; i0 < n; i0 += MATCH_THREADS * MATCH_BATCH) {
-        PointFetch pf[MATCH_BATCH];
-#pragma unroll
-        for (int j = 0; j < MATCH_BATCH; ++j) {
-            const int i = i0 + j * MATCH_THREADS;
-            if (i < n) {
-                const float2 p = pts[i];
-                point_fetch(cells, g, est[0], est[1], cs, sn, p.x * f, p.y * f, pf[j]);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < MATCH_BATCH; ++j)
-            if (i0 + j * MATCH_THREADS < n) point_accum(pf[j], cs, sn, acc);
-    }
-    wave_butterfly(acc);  // 64-lane xor butterfly, offsets 32..1
-    const int wave = tid >> 6;
-    if ((tid & 63) == 0) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) red[parity][wave][k] = acc[k];
-    }
-    __syncthreads();
     float s[9];
+    if constexpr (SEQ) {
+        const int cw = blockIdx.x & (MATCH_WAVES - 1);
+        float run = 0.0f;
+        for (int c0 = 0; c0 < n; c0 += MATCH_THREADS) {
+            const int i = c0 + tid;
+            float t[9];
+            if (i < n) {
+                PointFetch pf;
+                const float2 p = pts[i];
+                point_fetch(cells, g, est[0], est[1], cs, sn, p.x * f, p.y * f, pf);
+                point_terms(pf, cs, sn, t);
+            }
+            seq_chunk(seqT, t, i < n, c0 == 0, min(MATCH_THREADS, n - c0), cw, run);
+        }
+        if ((tid >> 6) == cw && (tid & 63) < 9) red[parity][0][tid & 63] = run;
+        __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        // xor butterfly over the 4 wave sums: off 2 then off 1
-        float a0 = red[parity][0][k] + red[parity][2][k];
-        float a1 = red[parity][1][k] + red[parity][3][k];
-        s[k] = a0 + a1;
+        for (int k = 0; k < 9; ++k) s[k] = red[parity][0][k];
+    } else {
+        float acc[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
+        // per-thread order of the points is i = tid, tid + 256, ... (the oracle's reduce_threads order)
+        for (int i0 = tid; i0 < n; i0 += MATCH_THREADS * MATCH_BATCH) {
+            PointFetch pf[MATCH_BATCH];
+#pragma unroll
+            for (int j = 0; j < MATCH_BATCH; ++j) {
+                const int i = i0 + j * MATCH_THREADS;
+                if (i < n) {
+                    const float2 p = pts[i];
+                    point_fetch(cells, g, est[0], est[1], cs, sn, p.x * f, p.y * f, pf[j]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < MATCH_BATCH; ++j)
+                if (i0 + j * MATCH_THREADS < n) point_accum(pf[j], cs, sn, acc);
+        }
+        wave_butterfly(acc);  // 64-lane xor butterfly, offsets 32..1
+        const int wave = tid >> 6;
+        if ((tid & 63) == 0) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) red[parity][wave][k] = acc[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            // xor butterfly over the 4 wave sums: off 2 then off 1
+            float a0 = red[parity][0][k] + red[parity][2][k];
+            float a1 = red[parity][1][k] + red[parity][3][k];
+            s[k] = a0 + a1;
+        }
     }
     float b[3] = {s[0], s[1], s[2]};
     H[0] = s[3]; H[4] = s[4]; H[8] = s[5];
@@ -405,16 +503,14 @@ constexpr unsigned NB_NONE = 0xFFFFFFFFu;
 // (s_pose[parity]: est[3], cos, sin, H[9], clamp flag); the other waves would only repeat it.
 constexpr int POSE_WORDS = 16;
 
-template <int NP>
+template <int NP, bool SEQ>
 __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
                                             int n, float f, float *est, float &cs, float &sn, float *H,
                                             float (*red)[MATCH_WAVES][9], int parity, unsigned *nb_key,
-                                            float4 *nb_val, unsigned short *mlist, float (*s_pose)[POSE_WORDS])
+                                            float4 *nb_val, unsigned short *mlist, float (*s_pose)[POSE_WORDS],
+                                            float *seqT)
 {
     const int tid = threadIdx.x;
-    float acc[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
     PointFetch pf[NP];
     unsigned key[NP];
     bool miss[NP];
@@ -482,31 +578,58 @@ __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, con
         nb_val[slot] = make_float4(cell_prob(v.x), cell_prob(v.y), cell_prob(v.z), cell_prob(v.w));
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        const int slot = tid + j * MATCH_THREADS;
-        if (slot >= n) continue;
-        if (pf[j].in) {
-            const float4 v = nb_val[slot];
-            pf[j].l[0] = v.x; pf[j].l[1] = v.y; pf[j].l[2] = v.z; pf[j].l[3] = v.w;
-        }
-        point_accum<true>(pf[j], cs, sn, acc);
-    }
-    wave_butterfly(acc);  // 64-lane xor butterfly, offsets 32..1
     const int wave = tid >> 6;
-    if ((tid & 63) == 0) {
+    const int cw = (int)(blockIdx.x & (MATCH_WAVES - 1));  // the chain / step-tail wave
+    float run = 0.0f;                                       // SEQ: lane k < 9 of wave cw: sum of term k
+    if constexpr (SEQ) {
+        // chunk j = points j * 256 .. j * 256 + 255 = slot j of every thread, in point order
 #pragma unroll
-        for (int k = 0; k < 9; ++k) red[parity][wave][k] = acc[k];
+        for (int j = 0; j < NP; ++j) {
+            if (j * MATCH_THREADS >= n) break;  // uniform
+            const int slot = tid + j * MATCH_THREADS;
+            float t[9];
+            if (slot < n) {
+                if (pf[j].in) {
+                    const float4 v = nb_val[slot];
+                    pf[j].l[0] = v.x; pf[j].l[1] = v.y; pf[j].l[2] = v.z; pf[j].l[3] = v.w;
+                }
+                point_terms<true>(pf[j], cs, sn, t);
+            }
+            seq_chunk(seqT, t, slot < n, j == 0, min(MATCH_THREADS, n - j * MATCH_THREADS), cw, run);
+        }
+    } else {
+        float acc[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            const int slot = tid + j * MATCH_THREADS;
+            if (slot >= n) continue;
+            if (pf[j].in) {
+                const float4 v = nb_val[slot];
+                pf[j].l[0] = v.x; pf[j].l[1] = v.y; pf[j].l[2] = v.z; pf[j].l[3] = v.w;
+            }
+            point_accum<true>(pf[j], cs, sn, acc);
+        }
+        wave_butterfly(acc);  // 64-lane xor butterfly, offsets 32..1
+        if ((tid & 63) == 0) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) red[parity][wave][k] = acc[k];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     float *sp = s_pose[parity];
-    if (wave == (int)(blockIdx.x & (MATCH_WAVES - 1))) {
+    if (wave == cw) {
         float s[9];
+        if constexpr (SEQ) {
+            seq_gather(run, s);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            float a0 = red[parity][0][k] + red[parity][2][k];
-            float a1 = red[parity][1][k] + red[parity][3][k];
-            s[k] = a0 + a1;
+            for (int k = 0; k < 9; ++k) {
+                float a0 = red[parity][0][k] + red[parity][2][k];
+                float a1 = red[parity][1][k] + red[parity][3][k];
+                s[k] = a0 + a1;
+            }
         }
         float b[3] = {s[0], s[1], s[2]};
         H[0] = s[3]; H[4] = s[4]; H[8] = s[5];
@@ -554,15 +677,20 @@ constexpr int MATCH_REG_PTS = 5;  // points per thread kept in registers: scans 
 #ifndef S2D_MATCH_WAVES
 #define S2D_MATCH_WAVES 1
 #endif
+// SEQ (default): H / b summed in the reference's sequential point order; else the tree order
+// (SLAM2D_MATCH_ORDER=tree / hs_set_reduction_order: faster, poses within float reassociation of the
+// reference's).
+template <bool SEQ>
 __global__ void __launch_bounds__(MATCH_THREADS) __attribute__((amdgpu_waves_per_eu(S2D_MATCH_WAVES)))
 hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__restrict__ state,
                 const float2 *__restrict__ xy, int xy_stride, const int *__restrict__ counts,
                 const float2 *__restrict__ origo, const float *__restrict__ hints, int stream_begin, int mode,
                 float *__restrict__ out_pose, float *__restrict__ out_cov, PoseLog plog, WorkQueue *__restrict__ wq,
-                UpdList *__restrict__ wl, IngestGeom ig, MatchIngest mi)
+                UpdList *__restrict__ wl, IngestGeom ig, MatchIngest mi, float2 *__restrict__ mc, int mc_stride)
 {
     static_assert(MATCH_THREADS == 64 * MATCH_WAVES && MATCH_WAVES == 4, "reduction tree assumes 4 waves");
     __shared__ float red[2][MATCH_WAVES][9];
+    __shared__ __attribute__((aligned(16))) float seqT[SEQ ? SEQ_WORDS : 4];  // SEQ: one chunk's terms
     __shared__ unsigned nb_key[MATCH_REG_PTS * MATCH_THREADS];
     __shared__ float4 nb_val[MATCH_REG_PTS * MATCH_THREADS];
     __shared__ unsigned short mlist[MATCH_REG_PTS * MATCH_THREADS];  // per wave: slots whose cell moved
@@ -615,6 +743,22 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             }
         }
         if (fused) __syncthreads();  // stage read before nb_val is written
+        // MapRepMultiMap keeps the scan it matched: dataContainers[l - 1].setFrom(container, 1 / 2^l)
+        // (MapRepMultiMap.h:161) is what updateByScan later draws into levels >= 1 (:187).  The stream's
+        // stored container (level-0 scale, scaled at use exactly as setFrom does) is mc[s]; the fused
+        // ingest already wrote the points there.
+        float2 *mcs = mc ? mc + (size_t)s * mc_stride : nullptr;
+        if (mcs && mcs != pts && geom.levels > 1) {
+            if (in_regs) {
+#pragma unroll
+                for (int j = 0; j < MATCH_REG_PTS; ++j) {
+                    const int i = threadIdx.x + j * MATCH_THREADS;
+                    if (i < n) mcs[i] = preg[j];
+                }
+            } else {
+                for (int i = threadIdx.x; i < n; i += MATCH_THREADS) mcs[i] = pts[i];
+            }
+        }
         for (int lvl = geom.levels - 1; lvl >= 0; --lvl) {
             const LevelGeom &g = geom.lv[lvl];
             const int iters = lvl == 0 ? 5 : 3;
@@ -627,11 +771,11 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             float cs = sdm_cosf(est[2]), sn = sdm_sinf(est[2]);
             for (int it = 0; it <= iters; ++it) {
                 if (in_regs) {
-                    gn_step_reg<MATCH_REG_PTS>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, red, parity, nb_key,
-                                               nb_val, mlist, s_pose);
+                    gn_step_reg<MATCH_REG_PTS, SEQ>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, red, parity, nb_key,
+                                                    nb_val, mlist, s_pose, seqT);
                     clamps += s_pose[parity][14] != 0.0f ? 1 : 0;
                 } else {
-                    gn_step(lc, g, pts, n, g.pts_scale, est, H, red, parity, &clamps);
+                    gn_step<SEQ>(lc, g, pts, n, g.pts_scale, est, H, red, parity, &clamps, seqT);
                 }
                 parity ^= 1;
             }
@@ -678,6 +822,11 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     const float2 org = fused ? ig.origo : (origo ? origo[local] : make_float2(0.0f, 0.0f));
     st.origo[0] = org.x;
     st.origo[1] = org.y;
+    if (mode == MODE_PROCESS || mode == MODE_MATCH_ONLY) {  // the stored container (see above)
+        st.mc_n = n;
+        st.mc_origo[0] = org.x;
+        st.mc_origo[1] = org.y;
+    }
     if (fused) {
         mi.n_out[local] = n;
         mi.origo_out[local] = org;
@@ -737,7 +886,7 @@ struct RayFrame {
     int bxi, byi;
 };
 
-__device__ __forceinline__ RayFrame ray_frame(const LevelGeom &g, const StreamState &st)
+__device__ __forceinline__ RayFrame ray_frame(const LevelGeom &g, const StreamState &st, const float *org)
 {
     RayFrame fr;
     float mp[3];
@@ -747,7 +896,7 @@ __device__ __forceinline__ RayFrame ray_frame(const LevelGeom &g, const StreamSt
     fr.cs = sdm_cosf(mp[2]);
     fr.sn = sdm_sinf(mp[2]);
     const float f = g.pts_scale;
-    float ox = st.origo[0] * f, oy = st.origo[1] * f;
+    float ox = org[0] * f, oy = org[1] * f;  // setFrom: origo * factor (DataPointContainer.h:48)
     float nsn = -fr.sn;
     float bx = fr.mx + (fr.cs * ox + nsn * oy);   // poseTransform * origo (:132)
     float by = fr.my + (fr.sn * ox + fr.cs * oy);
@@ -935,7 +1084,7 @@ __device__ __forceinline__ int block_exscan(int v, int *s_wave, int *total)
 
 __global__ void __launch_bounds__(BIN_THREADS)
 hs_bin_kernel(FleetGeom geom, StreamState *__restrict__ state, const float2 *__restrict__ xy, int xy_stride,
-              int stream_begin, int max_points, unsigned *__restrict__ rays_g, uint4 *__restrict__ segs,
+              const float2 *__restrict__ mc, int mc_stride, int stream_begin, int max_points, unsigned *__restrict__ rays_g, uint4 *__restrict__ segs,
               WorkItem *__restrict__ items, WorkItem *__restrict__ wholes, WorkQueue *__restrict__ wq,
               unsigned seg_cap, unsigned item_cap)
 {
@@ -949,15 +1098,16 @@ hs_bin_kernel(FleetGeom geom, StreamState *__restrict__ state, const float2 *__r
     const int s = stream_begin + local;
     const StreamState &st = state[s];
     if (!st.do_update) return;
-    const int n = st.n;
     const int tid = threadIdx.x;
-    const float2 *pts = xy + (size_t)local * xy_stride;
     unsigned long long Ltot = 0, Rtot = 0;
 
     for (int lvl = 0; lvl < geom.levels; ++lvl) {
         const LevelGeom &g = geom.lv[lvl];
+        // level 0: this step's DataContainer; levels >= 1: the stored one (MapRepMultiMap.h:181-188)
+        const int n = lvl == 0 ? st.n : st.mc_n;
+        const float2 *pts = lvl == 0 ? xy + (size_t)local * xy_stride : mc + (size_t)s * mc_stride;
         unsigned *rays = rays_g + ((size_t)s * geom.levels + lvl) * max_points;
-        const RayFrame fr = ray_frame(g, st);
+        const RayFrame fr = ray_frame(g, st, lvl == 0 ? st.origo : st.mc_origo);
         const int x0 = fr.bxi, y0 = fr.byi;
         if (tid == 0) {
             s_bbox[0] = x0; s_bbox[1] = y0; s_bbox[2] = x0; s_bbox[3] = y0;
@@ -1129,13 +1279,9 @@ __device__ unsigned long long g_stamps[8];
 #define S2D_STAMP(v) do { } while (0)
 #endif
 
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt) but not
+// lds_barrier (defined with the match kernel): waits for this wave's LDS operations (lgkmcnt) but not
 // for its global loads/stores (__syncthreads' release fence would also drain vmcnt, serialising the
 // prefetched cell loads and the previous tile's stores into every barrier).
-__device__ __forceinline__ void lds_barrier()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 // Tile kernel: ONE WAVE per workgroup and per tile, so there is no workgroup barrier and many tiles
 // are in flight per CU (latency, not issue, bounds this phase).  Workgroup w takes items w, w+G, ...
@@ -1446,8 +1592,9 @@ constexpr int UPD_RREG = 5;
 template <int RREG>
 __global__ void __launch_bounds__(UPD_THREADS, S2D_UPD_MINB)
 hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restrict__ state,
-                 const float2 *__restrict__ xy, int xy_stride, int stream_begin, int count, int max_points,
-                 const UpdList *__restrict__ wl, UpdList *__restrict__ wl_next, int ncu)
+                 const float2 *__restrict__ xy, int xy_stride, const float2 *__restrict__ mc, int mc_stride,
+                 int stream_begin, int count, int max_points, const UpdList *__restrict__ wl,
+                 UpdList *__restrict__ wl_next, int ncu)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned smem[];
     // two mark buffers (tile i rasters into buffer i & 1 while tile i - 1's cells are applied),
@@ -1488,11 +1635,13 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     const StreamState &st = state[s];
     if (!st.do_update) return;
     const LevelGeom &g = geom.lv[lvl];
-    const int n = st.n;
+    // level 0: this step's DataContainer; levels >= 1: the stored one of the last match
+    // (MapRepMultiMap::updateByScan, MapRepMultiMap.h:181-188; equal to this step's after a match)
+    const int n = lvl == 0 ? st.n : st.mc_n;
     const int tid = threadIdx.x;
     float *lvw = cells + (size_t)s * geom.stream_words + g.word_offset;
 
-    const RayFrame fr = ray_frame(g, st);
+    const RayFrame fr = ray_frame(g, st, lvl == 0 ? st.origo : st.mc_origo);
     const int x0 = fr.bxi, y0 = fr.byi;
     if (tid == 0) {
         s_bbox[0] = x0; s_bbox[1] = y0; s_bbox[2] = x0; s_bbox[3] = y0;
@@ -1500,7 +1649,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     __syncthreads();
     int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
     unsigned long long L = 0, R = 0;
-    const float2 *pts = xy + (size_t)local * xy_stride;
+    const float2 *pts = lvl == 0 ? xy + (size_t)local * xy_stride : mc + (size_t)s * mc_stride;
     for (int b0 = tid & ~63; (b0 & ~255) < n; b0 += UPD_THREADS) {   // wave-uniform trip count
         const int b = fan_beam(b0, lane);
         unsigned r = RAY_INVALID;

@@ -67,6 +67,8 @@ def _declare(L):
     L.hs_ingest_batch_device.argtypes = [_p, _i, _p, _i, _p, _i, _p, _p, _p]
     L.hs_step_ranges_batch_device.argtypes = [_p, _i, _i, _p, _i, _p, _p]
     L.hs_update_ranges.argtypes = [_p, _i, _p, _p, _p, P(_i)]
+    L.hs_set_reduction_order.argtypes = [_p, _i]
+    L.hs_get_reduction_order.argtypes = [_p, P(_i)]
     # GMapping particle path (include/slam2d/gmapping.h)
     D = C.c_double
     L.gm_version.restype = C.c_char_p

@@ -154,8 +154,42 @@ def normalize_weights(scores, group=None):
     return w, float(neff)
 
 
+NCCL_UNIQUE_ID_BYTES = 128  # rccl.h
+
+
 class _UniqueId(C.Structure):
-    _fields_ = [("internal", C.c_char * 128)]   # ncclUniqueId (rccl.h: NCCL_UNIQUE_ID_BYTES)
+    # ncclUniqueId {char internal[NCCL_UNIQUE_ID_BYTES]}: raw bytes (a random magic + a sockaddr, so it
+    # holds NUL bytes) -- an unsigned byte array, never a C string
+    _fields_ = [("internal", C.c_uint8 * NCCL_UNIQUE_ID_BYTES)]
+
+
+def unique_id_bytes(uid: _UniqueId) -> np.ndarray:
+    """All NCCL_UNIQUE_ID_BYTES bytes of an ncclUniqueId as uint8 (a c_char array field would stop at the
+    first NUL: ctypes reads c_char arrays as C strings)."""
+    b = C.string_at(C.addressof(uid), C.sizeof(uid))
+    assert len(b) == NCCL_UNIQUE_ID_BYTES
+    return np.frombuffer(b, np.uint8).copy()
+
+
+def unique_id_from_bytes(buf) -> _UniqueId:
+    buf = np.ascontiguousarray(buf, np.uint8).reshape(-1)
+    if buf.size != NCCL_UNIQUE_ID_BYTES:
+        raise Slam2dError(f"ncclUniqueId must be {NCCL_UNIQUE_ID_BYTES} bytes, got {buf.size}")
+    uid = _UniqueId()
+    C.memmove(C.addressof(uid), buf.tobytes(), NCCL_UNIQUE_ID_BYTES)
+    return uid
+
+
+def exchange_unique_id(uid: _UniqueId | None, world: int, rank: int, bcast) -> _UniqueId:
+    """Rank 0's ncclUniqueId on every rank: bcast(uint8[128]) broadcasts rank 0's array (e.g. over
+    torch.distributed); every rank checks that all 128 bytes arrived."""
+    if world <= 1:
+        return uid
+    buf = unique_id_bytes(uid) if rank == 0 else np.zeros(NCCL_UNIQUE_ID_BYTES, np.uint8)
+    out = np.asarray(bcast(buf), np.uint8).reshape(-1)
+    if out.size != NCCL_UNIQUE_ID_BYTES:
+        raise Slam2dError(f"unique id broadcast returned {out.size} bytes, expected {NCCL_UNIQUE_ID_BYTES}")
+    return unique_id_from_bytes(out)
 
 
 class RcclComm:
@@ -173,10 +207,7 @@ class RcclComm:
         uid = _UniqueId()
         if rank == 0:
             self._ok(self._R.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
-        if world > 1:
-            buf = np.frombuffer(bytes(uid.internal), np.uint8).copy() if rank == 0 else np.zeros(128, np.uint8)
-            buf = bcast(buf)
-            C.memmove(C.addressof(uid), buf.tobytes(), 128)
+        uid = exchange_unique_id(uid, int(world), int(rank), bcast)
         h = C.c_void_p()
         self._ok(self._R.ncclCommInitRank(C.byref(h), int(world), uid, int(rank)), "ncclCommInitRank")
         self.handle = h.value

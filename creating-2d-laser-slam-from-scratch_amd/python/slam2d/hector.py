@@ -136,6 +136,17 @@ class HectorFleet:
     def set_thresholds(self, min_dist: float, min_angle: float):
         check(self.L.hs_set_map_update_thresholds(self.h, _f(min_dist), _f(min_angle)), "hs_set_map_update_thresholds")
 
+    ORDER_REFERENCE = 0   # H / b summed in point order, as OccGridMapUtil.h:94-126 (default)
+    ORDER_TREE256 = 256   # 256-thread tree (faster; the oracle's reduce_threads=256)
+
+    def set_reduction_order(self, order: int):
+        check(self.L.hs_set_reduction_order(self.h, int(order)), "hs_set_reduction_order")
+
+    def reduction_order(self) -> int:
+        o = C.c_int()
+        check(self.L.hs_get_reduction_order(self.h, C.byref(o)), "hs_get_reduction_order")
+        return o.value
+
     # ---------------------------------------------------------------- single-stream (host buffers)
     def update(self, stream: int, pts, origo=(0.0, 0.0), hint=None, map_without_matching=False):
         pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)

@@ -56,7 +56,9 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
               float map_start_x, float map_start_y, int levels, int max_points);
 /* ~HectorSlamProcessor (HectorSlamProcessor.h:70-73) */
 int hs_destroy(hs_ctx *ctx);
-/* HectorSlamProcessor::reset (HectorSlamProcessor.h:111-117) for every stream */
+/* HectorSlamProcessor::reset (HectorSlamProcessor.h:111-117) for every stream: grids cleared, pose and
+ * last-map-update pose reset; the update indices, the last covariance and the stored containers are
+ * kept, as in the reference (GridMapBase::reset clears cells only, MapRepMultiMap::reset the maps only). */
 int hs_reset(hs_ctx *ctx);
 /* MapRepresentationInterface::setUpdateFactorFree / setUpdateFactorOccupied (:67-68) */
 int hs_set_update_factors(hs_ctx *ctx, float free_factor, float occupied_factor);
@@ -75,10 +77,14 @@ int hs_get_map_info(hs_ctx *ctx, int level, int *size_x, int *size_y, float *cel
  * did_update_out may be NULL. */
 int hs_update(hs_ctx *ctx, int stream, const float *xy, int n, float ox, float oy, const float *hint,
               int map_without_matching, float pose_out[3], float cov_out[9], int *did_update_out);
-/* MapRepresentationInterface::matchData (MapRepMultiMap.h:144-167): no state change */
+/* MapRepresentationInterface::matchData (MapRepMultiMap.h:144-167): no pose / map change; like the
+ * reference it keeps the matched DataContainer (dataContainers[l-1].setFrom, :161), which a later
+ * hs_update_by_scan / hs_update(map_without_matching) draws into levels >= 1 (:187). */
 int hs_match(hs_ctx *ctx, int stream, const float *xy, int n, float ox, float oy, const float hint[3],
              float pose_out[3], float cov_out[9]);
-/* MapRepresentationInterface::updateByScan + onMapUpdated (MapRepMultiMap.h:174-191, :127-135) */
+/* MapRepresentationInterface::updateByScan + onMapUpdated (MapRepMultiMap.h:174-191, :127-135): level 0
+ * from (xy, n, ox, oy); levels >= 1 from the container of the stream's last match (empty before the
+ * first one), exactly as MapRepMultiMap::updateByScan does. */
 int hs_update_by_scan(hs_ctx *ctx, int stream, const float *xy, int n, float ox, float oy, const float pose[3]);
 
 /* HectorSlamProcessor::getLastScanMatchPose / getLastScanMatchCovariance (HectorSlamProcessor.h:120-122) */
@@ -175,6 +181,16 @@ int hs_set_pose_log(hs_ctx *ctx, float *d_buf, int streams, int capacity);
 int hs_set_pose_log_slots(hs_ctx *ctx, float *d_buf, const int *d_slot_of_stream, int slots, int capacity);
 /* The context's own HIP stream (hipStream_t as void*). */
 void *hs_get_stream(hs_ctx *ctx);
+
+/* ---- Hessian summation order of the matcher -------------------------------------------------------
+ * HS_ORDER_REFERENCE (default): H and dTr summed point after point as getCompleteHessianDerivs does
+ * (OccGridMapUtil.h:94-126) -- poses equal the reference's evaluation order bit for bit.
+ * HS_ORDER_TREE256: per-thread strided partials + xor butterflies (faster; float reassociation of the
+ * same sums).  SLAM2D_MATCH_ORDER=tree in the environment at hs_create selects it too. */
+#define HS_ORDER_REFERENCE 0
+#define HS_ORDER_TREE256 256
+int hs_set_reduction_order(hs_ctx *ctx, int order);
+int hs_get_reduction_order(hs_ctx *ctx, int *order_out);
 
 /* ---- measurement ----------------------------------------------------------------------------- */
 /* Kernel timing with HIP events recorded on the launch stream around every kernel of every step

@@ -77,6 +77,13 @@ typedef struct {
     int valid_rays;
     int clamp_count;
     float *red;                    /* scratch for tree-order emulation: T*9 floats */
+    /* MapRepMultiMap::dataContainers (MapRepMultiMap.h:89): the DataContainer of the last matchData
+     * (setFrom at :161), drawn into levels >= 1 by updateByScan (:187).  Kept at level-0 scale; the
+     * level's factor is applied at use, the same float product setFrom computes
+     * (DataPointContainer.h:46-58).  Empty until the first match; reset() keeps it (:102-110). */
+    float *mc_xy;
+    int mc_n, mc_cap;
+    float mc_origo[2];
     /* per-iteration trace (optional, for fixtures) */
     float *trace;                  /* [max_trace][3+9+3] pose-before, H(9) ... */
     int trace_cap, trace_len;
@@ -227,10 +234,12 @@ void ho_destroy(ho_ctx *c)
     for (int i = 0; i < c->levels; ++i) free(c->lv[i].cells);
     free(c->red);
     free(c->trace);
+    free(c->mc_xy);
     free(c);
 }
 
-/* HectorSlamProcessor::reset -> MapRepMultiMap::reset -> MapProcContainer::reset */
+/* HectorSlamProcessor::reset -> MapRepMultiMap::reset -> MapProcContainer::reset (cells only: the grids'
+ * update indices, lastScanMatchCov and the stored containers are kept) */
 void ho_reset(ho_ctx *c)
 {
     c->last_map_update_pose[0] = c->last_map_update_pose[1] = c->last_map_update_pose[2] = FLT_MAX;
@@ -449,8 +458,21 @@ static void ho_match_level(ho_ctx *c, int lvl, const float *hint, const float *x
 }
 
 /* MapRepMultiMap::matchData  H/slam_main/MapRepMultiMap.h:144-167 */
-void ho_match(ho_ctx *c, const float *xy, int n, const float *hint, float *pose_out, float *cov_out)
+void ho_match(ho_ctx *c, const float *xy, int n, float ox, float oy, const float *hint, float *pose_out,
+              float *cov_out)
 {
+    /* dataContainers[index-1].setFrom(dataContainer, 1/2^index)  :161 (every level >= 1, every call) */
+    if (c->levels > 1) {
+        if (n > c->mc_cap) {
+            free(c->mc_xy);
+            c->mc_cap = n;
+            c->mc_xy = (float *)malloc(sizeof(float) * 2 * (size_t)n);
+        }
+        if (n > 0) memcpy(c->mc_xy, xy, sizeof(float) * 2 * (size_t)n);
+        c->mc_n = n;
+        c->mc_origo[0] = ox;
+        c->mc_origo[1] = oy;
+    }
     float tmp[3] = {hint[0], hint[1], hint[2]};
     for (int lvl = c->levels - 1; lvl >= 0; --lvl) {
         float o[3];
@@ -563,7 +585,10 @@ void ho_update_by_scan(ho_ctx *c, const float *xy, int n, float ox, float oy, co
     c->sum_L = 0;
     c->sum_free = 0;
     c->valid_rays = 0;
-    for (int lvl = 0; lvl < c->levels; ++lvl) ho_update_level(c, lvl, xy, n, ox, oy, world_pose);
+    for (int lvl = 0; lvl < c->levels; ++lvl) {
+        if (lvl == 0) ho_update_level(c, lvl, xy, n, ox, oy, world_pose);         /* :181-184 */
+        else ho_update_level(c, lvl, c->mc_xy, c->mc_n, c->mc_origo[0], c->mc_origo[1], world_pose);  /* :187 */
+    }
 }
 
 /* HectorSlamProcessor::update  H/slam_main/HectorSlamProcessor.h:81-108 ; returns 1 if the map was updated */
@@ -572,7 +597,7 @@ int ho_process(ho_ctx *c, const float *xy, int n, float ox, float oy, const floa
 {
     float np[3];
     if (!map_without_matching) {
-        ho_match(c, xy, n, hint, np, c->last_cov);
+        ho_match(c, xy, n, ox, oy, hint, np, c->last_cov);
     } else {
         np[0] = hint[0]; np[1] = hint[1]; np[2] = hint[2];
     }
@@ -595,6 +620,7 @@ int ho_process(ho_ctx *c, const float *xy, int n, float ox, float oy, const floa
 /* ------------------------------------------------------------------------------------------ */
 /* accessors */
 void ho_get_last_pose(const ho_ctx *c, float *pose) { memcpy(pose, c->last_scan_match_pose, sizeof(float) * 3); }
+void ho_get_last_cov(const ho_ctx *c, float *cov) { memcpy(cov, c->last_cov, sizeof(float) * 9); }
 int ho_levels(const ho_ctx *c) { return c->levels; }
 void ho_level_dims(const ho_ctx *c, int lvl, int *sx, int *sy) { *sx = c->lv[lvl].sx; *sy = c->lv[lvl].sy; }
 void ho_get_level(const ho_ctx *c, int lvl, float *l_out, int *upd_out)

@@ -59,11 +59,12 @@ def hector_lib(variant: str = "") -> C.CDLL:
         L.ho_enable_trace.argtypes = [_p, _i]
         L.ho_trace_len.argtypes = [_p]
         L.ho_get_trace.argtypes = [_p, _p]
-        L.ho_match.argtypes = [_p, _p, _i, _p, _p, _p]
+        L.ho_match.argtypes = [_p, _p, _i, _f, _f, _p, _p, _p]
         L.ho_update_by_scan.argtypes = [_p, _p, _i, _f, _f, _p]
         L.ho_process.restype = _i
         L.ho_process.argtypes = [_p, _p, _i, _f, _f, _p, _i, _p, _p]
         L.ho_get_last_pose.argtypes = [_p, _p]
+        L.ho_get_last_cov.argtypes = [_p, _p]
         L.ho_level_dims.argtypes = [_p, _i, C.POINTER(_i), C.POINTER(_i)]
         L.ho_get_level.argtypes = [_p, _i, _p, _p]
         L.ho_set_level.argtypes = [_p, _i, _p, _p]
@@ -138,12 +139,13 @@ class HectorOracle:
                                 1 if map_without_matching else 0, _fp(pose), _fp(cov))
         return pose, cov.reshape(3, 3), bool(did)
 
-    def match(self, pts, hint):
+    def match(self, pts, hint, origo=(0.0, 0.0)):
+        """MapRepMultiMap::matchData: pose + cov; keeps the container for levels >= 1 (:161)."""
         pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 2)
         hint = np.asarray(hint, np.float32)
         pose = np.zeros(3, np.float32)
         cov = np.zeros(9, np.float32)
-        self.L.ho_match(self.h, _fp(pts), pts.shape[0], _fp(hint), _fp(pose), _fp(cov))
+        self.L.ho_match(self.h, _fp(pts), pts.shape[0], _f(origo[0]), _f(origo[1]), _fp(hint), _fp(pose), _fp(cov))
         return pose, cov.reshape(3, 3)
 
     def update_by_scan(self, pts, pose, origo=(0.0, 0.0)):
@@ -155,6 +157,12 @@ class HectorOracle:
         p = np.zeros(3, np.float32)
         self.L.ho_get_last_pose(self.h, _fp(p))
         return p
+
+    def last_cov(self):
+        """HectorSlamProcessor::getLastScanMatchCovariance (HectorSlamProcessor.h:122)."""
+        cv = np.zeros(9, np.float32)
+        self.L.ho_get_last_cov(self.h, _fp(cv))
+        return cv.reshape(3, 3)
 
     def dims(self, lvl):
         sx, sy = _i(), _i()

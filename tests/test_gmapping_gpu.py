@@ -171,8 +171,9 @@ def test_normalize_weights_rccl_world1(gpu, use_comm):
     """gm_normalize_weights_device: the C-ABI form of the particle-weight exchange, with a real RCCL
     communicator made as a C++ host would (ncclGetUniqueId + ncclCommInitRank, world size 1 on the one
     GPU of the box) or none.  Sums are exact integers in double, weights equal the Python
-    normalize_weights (torch) bit for bit; the world-2 exchange itself is covered with gloo
-    (tests/test_host_cpu.py)."""
+    normalize_weights (torch) bit for bit.  On the CPU (gloo, world 2): RcclComm's unique-id broadcast
+    with NUL bytes (test_rccl_unique_id_with_nul_bytes_gloo_world2) and the sums' algebra
+    (test_particle_weight_allreduce_gloo_world2); sharding itself: test_sharded_fleet_equals_unsharded."""
     import torch
 
     from slam2d.gmapping import RcclComm, normalize_weights
@@ -195,3 +196,61 @@ def test_normalize_weights_rccl_world1(gpu, use_comm):
     wt, neff = normalize_weights(scores)
     np.testing.assert_array_equal(w.cpu().numpy(), wt.cpu().numpy())
     assert neff == pytest.approx(s.sum() ** 2 / (s * s).sum(), rel=1e-15)
+
+
+@pytest.mark.parametrize("shards", [2, 8])
+def test_sharded_fleet_equals_unsharded(gpu, shards):
+    """P = 1024 particles split into `shards` GMappingFleet shards (what each of the
+    ranks of `bench.py --config gmapping --gpus N` holds) give every particle the same map (n, visits,
+    acc), score, hit and free counts as the unsharded fleet (GMapping::ComputeMap per particle,
+    gmapping.cc:171-242), and combining the shards' exchange words [Σ(s+1), Σ(s+1)^2] -- what the RCCL
+    all-reduce sums -- reproduces the unsharded gm_normalize_weights_device weights bit for bit."""
+    import torch
+
+    P, T = 1024, 2
+    ang = synth.beam_angles().astype(np.float64)
+    segs = synth.world_segments()
+    gt = synth.trajectory(T, 0.0)
+    rng = np.random.default_rng(4242)
+    noise = rng.normal(0, [0.05, 0.05, 0.02], size=(P, 3))
+    ranges = [synth.cast_ranges(gt[t:t + 1], segs)[0].astype(np.float32) for t in range(T)]
+    hs = torch.cuda.current_stream().cuda_stream
+
+    def run(lo, hi):
+        f = GMappingFleet(hi - lo)
+        f.set_beams(ang)
+        d_sc = torch.zeros(hi - lo, dtype=torch.int32, device="cuda")
+        for t in range(T):
+            d_p = torch.from_numpy(GMappingFleet.poses4(gt[t] + noise[lo:hi])).cuda()
+            d_r = torch.from_numpy(ranges[t]).cuda()
+            f.compute_device(d_p.data_ptr(), d_r.data_ptr(), len(ranges[t]), d_sc.data_ptr(), hip_stream=hs)
+        w = torch.zeros(hi - lo, dtype=torch.float64, device="cuda")
+        sums = torch.zeros(2, dtype=torch.float64, device="cuda")
+        f.normalize_weights_device(None, d_sc.data_ptr(), hi - lo, w.data_ptr(), sums.data_ptr(), hip_stream=hs)
+        torch.cuda.synchronize()
+        return f, f.scores(), w.cpu().numpy(), sums.cpu().numpy()
+
+    full, (s0, h0, f0), w0, sums0 = run(0, P)
+    assert s0.sum() > 0 and (h0 > 0).all()
+    sample = {}
+    bounds = np.linspace(0, P, shards + 1).astype(int)
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        for p in (lo, hi - 1, (lo + hi) // 2):
+            sample[p] = full.particle_map(p)
+    full.close()
+    tot = np.zeros(2)
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        f, (s, h, fr), _, sums = run(lo, hi)
+        np.testing.assert_array_equal(s, s0[lo:hi])
+        np.testing.assert_array_equal(h, h0[lo:hi])
+        np.testing.assert_array_equal(fr, f0[lo:hi])
+        for p in (lo, hi - 1, (lo + hi) // 2):
+            n, v, acc = f.particle_map(p - lo)
+            np.testing.assert_array_equal(n, sample[p][0], err_msg=f"particle {p} n")
+            np.testing.assert_array_equal(v, sample[p][1], err_msg=f"particle {p} visits")
+            np.testing.assert_array_equal(acc.view(np.int32), sample[p][2].view(np.int32), err_msg=f"particle {p} acc")
+        f.close()
+        tot += sums  # the all-reduce: integer-valued doubles, exact in any order
+    np.testing.assert_array_equal(tot, sums0)
+    w_sharded = (s0.astype(np.float64) + 1.0) / tot[0]   # gm_weights_kernel with the all-reduced sums
+    np.testing.assert_array_equal(w_sharded.view(np.int64), w0.view(np.int64))

@@ -3,10 +3,11 @@
 Bar (BASELINE.json north_star):
   * integer / byte work bit-exact: every cell's updateIndex, the Bresenham cell count ΣL, the
     did-update gate, the map update index;
-  * log-odds floats bit-exact against the oracle run in the kernel's reduction order
-    (reduce_threads=256), because the update replays the reference's per-cell float sequence;
-  * pose within POSE_TOL_M / POSE_TOL_RAD of the oracle in the reference's sequential order
-    (the Hessian sums are reassociated by the parallel reduction).
+  * poses, covariances and log-odds floats bit-exact against the oracle in the reference's sequential
+    Hessian summation order (reduce_threads=0, OccGridMapUtil.h:94-126), which is the kernel's default
+    (HS_ORDER_REFERENCE): the north star's pose bar (<= 1e-4 m / rad) holds by construction;
+  * the opt-in tree order (HS_ORDER_TREE256) bit-exact against the oracle's reduce_threads=256 and
+    within POSE_TOL_M / POSE_TOL_RAD of the reference order.
 """
 import os
 
@@ -21,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 POSE_TOL_M = 1e-4    # north_star: pose error <= 1e-4 m
 POSE_TOL_RAD = 1e-4  # north_star: pose error <= 1e-4 rad
-T_RED = 256          # hs_match_kernel workgroup size (reduction order)
+T_RED = 0            # the oracle in the reference summation order == the kernel default (HS_ORDER_REFERENCE)
 
 
 def _bits(a):
@@ -99,23 +100,31 @@ def test_binned_path_bitexact(gpu, scans, monkeypatch, parts):
     assert q["whole"] == 0 and q["overflow"] == 0 and q["items"] > 0, q
 
 
-def test_pose_tolerance_vs_reference_order(gpu, scans):
-    """GPU trajectory vs the oracle in the reference's sequential summation order."""
+def test_tree_order_opt_in(gpu, scans):
+    """HS_ORDER_TREE256: bit-exact vs the oracle's tree order, within the pose tolerance of the reference
+    order; switching back restores the reference order."""
     n = 30
     fleet = HectorFleet(1, 0.05, 2048, (0.5, 0.5), 3, max_points=1081)
-    fleet.set_update_factors(0.4, 0.9)
-    fleet.set_thresholds(0.4, 0.9)
+    assert fleet.reduction_order() == HectorFleet.ORDER_REFERENCE
+    fleet.set_reduction_order(HectorFleet.ORDER_TREE256)
+    assert fleet.reduction_order() == HectorFleet.ORDER_TREE256
+    tree = O.HectorOracle(0.05, 2048, (0.5, 0.5), 3, reduce_threads=256)
     ref = O.HectorOracle(0.05, 2048, (0.5, 0.5), 3, reduce_threads=0)
-    ref.set_update_factors(0.4, 0.9)
-    ref.set_thresholds(0.4, 0.9)
+    for f in (fleet, tree, ref):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(0.4, 0.9)
     errs = []
     for k in range(n):
         pts = scans.points[0, k, : scans.counts[0, k]]
         gp, _, _ = fleet.update(0, pts)
+        tp, _, _ = tree.process(pts)
         rp, _, _ = ref.process(pts)
+        np.testing.assert_array_equal(_bits(gp), _bits(tp), err_msg=f"scan {k}")
         errs.append(np.abs(gp.astype(np.float64) - rp.astype(np.float64)))
     e = np.max(errs, axis=0)
     assert e[0] <= POSE_TOL_M and e[1] <= POSE_TOL_M and e[2] <= POSE_TOL_RAD, e
+    with pytest.raises(Exception):
+        fleet.set_reduction_order(128)
 
 
 def test_match_only_and_update_by_scan(gpu, scans):
@@ -165,6 +174,85 @@ def test_map_without_matching_and_empty_scan(gpu, scans):
     np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))
 
 
+def _same_levels(fleet, ora, levels, what=""):
+    for lvl in range(levels):
+        m = fleet.get_map(0, lvl)
+        ol, ou = ora.level(lvl)
+        np.testing.assert_array_equal(m["upd"], ou, err_msg=f"{what} level {lvl} updateIndex")
+        np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol), err_msg=f"{what} level {lvl} log-odds")
+        assert m["update_index"] == ora.update_index(lvl), (what, lvl)
+
+
+@pytest.mark.parametrize("levels", [2, 3])
+def test_map_without_matching_stored_containers(gpu, scans, levels):
+    """MapRepMultiMap keeps the container of the last matchData (setFrom, MapRepMultiMap.h:161) and
+    updateByScan draws THAT into levels >= 1 (:187): HectorSlamProcessor::update(map_without_matching)
+    updates level 0 with the new scan and the coarse levels with the previously matched one -- nothing at
+    all before the first match.  Bit-exact vs the oracle, which keeps the same state."""
+    size = 1024
+    fleet = HectorFleet(1, 0.05, size, (0.5, 0.5), levels, max_points=1081)
+    ora = O.HectorOracle(0.05, size, (0.5, 0.5), levels, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(0.4, 0.9)
+    hint = np.array([0.1, -0.05, 0.02], np.float32)
+    a = scans.points[1, 0, : scans.counts[1, 0]]
+    b = scans.points[1, 5, : scans.counts[1, 5]]
+    c = scans.points[2, 9, : scans.counts[2, 9]]
+    # first call: no match yet, the coarse levels get an empty container (index advance only)
+    gp, _, gd = fleet.update(0, a, origo=(0.5, -0.25), hint=hint, map_without_matching=True)
+    op, _, od = ora.process(a, origo=(0.5, -0.25), hint=hint, map_without_matching=True)
+    assert gd and od
+    np.testing.assert_array_equal(_bits(gp), _bits(op))
+    _same_levels(fleet, ora, levels, "first call")
+    assert (fleet.get_map(0, 1)["upd"] >= 0).sum() == 0  # nothing drawn into level 1
+    # a match of scan b (own origo), then map_without_matching with scan c: coarse levels draw b
+    gp, gc = fleet.match(0, b, hint, origo=(-0.75, 0.3))
+    op, oc = ora.match(b, hint, origo=(-0.75, 0.3))
+    np.testing.assert_array_equal(_bits(gp), _bits(op))
+    np.testing.assert_array_equal(_bits(gc), _bits(oc))
+    pose = np.array([0.3, 0.2, -0.4], np.float32)
+    for k in range(2):
+        gp, _, gd = fleet.update(0, c, hint=pose, map_without_matching=True)
+        op, _, od = ora.process(c, hint=pose, map_without_matching=True)
+        assert gd and od
+        np.testing.assert_array_equal(_bits(gp), _bits(op))
+        _same_levels(fleet, ora, levels, f"after match, call {k}")
+    # a full update (match + gate) re-stores its own scan
+    gp, _, gd = fleet.update(0, a)
+    op, _, od = ora.process(a)
+    assert gd == od
+    np.testing.assert_array_equal(_bits(gp), _bits(op))
+    gp, _, _ = fleet.update(0, b, hint=pose, map_without_matching=True)
+    op, _, _ = ora.process(b, hint=pose, map_without_matching=True)
+    _same_levels(fleet, ora, levels, "after a full update")
+
+
+def test_update_by_scan_after_match_of_other_scan(gpu, scans):
+    """hs_update_by_scan after hs_match on different data: level 0 from the given scan, levels >= 1 from
+    the matched one (MapRepMultiMap.h:174-191)."""
+    levels = 3
+    fleet = HectorFleet(1, 0.05, 1024, (0.5, 0.5), levels, max_points=1081)
+    ora = O.HectorOracle(0.05, 1024, (0.5, 0.5), levels, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+    # before any match: coarse levels untouched
+    a = scans.points[3, 2, : scans.counts[3, 2]]
+    pose = np.array([0.05, 0.02, 0.1], np.float32)
+    fleet.update_by_scan(0, a, pose, origo=(0.1, 0.1))
+    ora.update_by_scan(a, pose, origo=(0.1, 0.1))
+    _same_levels(fleet, ora, levels, "before a match")
+    for k in range(4):
+        m = scans.points[0, k, : scans.counts[0, k]]
+        u = scans.points[3, 10 + k, : scans.counts[3, 10 + k]]
+        gp, _ = fleet.match(0, m, pose, origo=(0.2 * k, -0.1))
+        op, _ = ora.match(m, pose, origo=(0.2 * k, -0.1))
+        np.testing.assert_array_equal(_bits(gp), _bits(op))
+        fleet.update_by_scan(0, u, op, origo=(-0.3, 0.05 * k))
+        ora.update_by_scan(u, op, origo=(-0.3, 0.05 * k))
+        _same_levels(fleet, ora, levels, f"round {k}")
+
+
 def test_degenerate_rays(gpu):
     """Zero-length beams (begin == end, skipped), 1-cell rays, rays along axes and diagonals."""
     pts = []
@@ -190,13 +278,36 @@ def test_degenerate_rays(gpu):
 
 
 def test_reset(gpu, scans):
-    fleet = HectorFleet(1, 0.05, 256, (0.5, 0.5), 1, max_points=1081)
-    pts = scans.points[0, 0, : scans.counts[0, 0]]
-    fleet.update(0, pts)
+    """HectorSlamProcessor::reset (HectorSlamProcessor.h:111-117): grids cleared and poses reset; the grids'
+    update indices (GridMapBase::reset clears cells only), the covariance and the stored containers stay
+    -- so later updates index cells exactly as the reference does."""
+    fleet = HectorFleet(1, 0.05, 256, (0.5, 0.5), 2, max_points=1081)
+    ora = O.HectorOracle(0.05, 256, (0.5, 0.5), 2, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(-1.0, -1.0)
+    for k in range(3):
+        pts = scans.points[0, k, : scans.counts[0, k]]
+        fleet.update(0, pts)
+        ora.process(pts)
     fleet.reset()
+    ora.reset()
     m = fleet.get_map(0, 0)
-    assert np.all(m["logodds"] == 0.0) and np.all(m["upd"] == -1) and m["update_index"] == -1
+    assert np.all(m["logodds"] == 0.0) and np.all(m["upd"] == -1)
+    assert m["update_index"] == ora.update_index(0) == 2
     assert np.all(fleet.last_pose(0)[0] == 0.0)
+    np.testing.assert_array_equal(_bits(fleet.last_pose(0)[1]), _bits(ora.last_cov()))
+    # map_without_matching right after reset: coarse level draws the container stored before it
+    pts = scans.points[0, 4, : scans.counts[0, 4]]
+    hint = np.array([0.02, 0.01, 0.0], np.float32)
+    fleet.update(0, pts, hint=hint, map_without_matching=True)
+    ora.process(pts, hint=hint, map_without_matching=True)
+    for k in range(5, 8):
+        pts = scans.points[0, k, : scans.counts[0, k]]
+        gp, _, _ = fleet.update(0, pts)
+        op, _, _ = ora.process(pts)
+        np.testing.assert_array_equal(_bits(gp), _bits(op))
+    _same_levels(fleet, ora, 2, "after reset")
 
 
 def test_processor_mirror(gpu, scans):
@@ -272,14 +383,16 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 @pytest.mark.parametrize("name", sorted(f for f in os.listdir(GOLD) if f.startswith("hector_")))
 def test_golden_fixture(gpu, name):
     """Committed oracle fixtures (tests/golden, oracle/make_golden.py) replayed through the C-ABI.
-    Fixtures in the GPU reduction order (reduce_threads 256) must match bit for bit (NaN == NaN for the
-    diverging case); the sequential-order fixture within the north-star pose tolerance."""
+    The fleet runs in the fixture's summation order (reference sequential / tree 256); everything must
+    match bit for bit (NaN == NaN for the diverging case)."""
     d = np.load(os.path.join(GOLD, name))
     levels, size = int(d["levels"]), int(d["size"])
     fleet = HectorFleet(1, 0.05, size, (0.5, 0.5), levels, max_points=1081)
     fleet.set_update_factors(0.4, 0.9)
     fleet.set_thresholds(*[float(v) for v in d["thresholds"]])
-    exact = int(d["reduce_threads"]) == T_RED
+    # the fixture's summation order: reference (0) by default, the tree (256) opt-in
+    fleet.set_reduction_order(int(d["reduce_threads"]))
+    exact = True
     for k in range(len(d["counts"])):
         gp, gc, gd = fleet.update(0, d["points"][k, : d["counts"][k]])
         if exact:

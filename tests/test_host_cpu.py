@@ -1,5 +1,6 @@
 """Host logic on the CPU: the DataContainer mirror, the synthetic scan generator, bench.py's
 accounting helpers, and bench's rank aggregation over torch.distributed (gloo, world_size 2)."""
+import ctypes as C
 import json
 import math
 import os
@@ -88,12 +89,20 @@ def test_kernel_symbol():
 
 
 def test_pmc_traffic_lookup(tmp_path, monkeypatch):
+    """roofline.traffic is attached only from a summary of the SAME workload (config, streams, map-update
+    semantics, summation order) and only when its launch time agrees with this run's (same build)."""
     p = tmp_path / "pmc.json"
-    p.write_text(json.dumps({"entries": [{"kernel": "hs_update_kernel", "config": "northstar", "streams": 1024,
-                                          "traffic_bytes_per_launch": 123, "source": "x"}]}))
+    e = {"kernel": "hs_update_kernel<5>", "config": "northstar", "streams": 1024, "semantics": "forced", "order": 0,
+         "avg_ns": 1000.0, "traffic_bytes_per_launch": 123, "source": "x"}
+    p.write_text(json.dumps({"entries": [e]}))
     monkeypatch.setattr(bench, "PMC_SUMMARY", str(p))
-    assert bench.pmc_traffic("hs_update_kernel", "northstar", 1024)["traffic_bytes_per_launch"] == 123
-    assert bench.pmc_traffic("hs_update_kernel", "c2", 1024) is None
+    w = {"config": "northstar", "streams": 1024, "semantics": "forced", "order": 0}
+    got, why = bench.pmc_traffic("hs_update_kernel", w, 1100.0)
+    assert got["traffic_bytes_per_launch"] == 123 and why == "x"
+    for k, v in (("config", "c2"), ("streams", 2048), ("semantics", "reference"), ("order", 256)):
+        assert bench.pmc_traffic("hs_update_kernel", {**w, k: v}, 1000.0)[0] is None, k
+    got, why = bench.pmc_traffic("hs_update_kernel", w, 2000.0)   # another build: refused
+    assert got is None and "another build" in why
 
 
 def test_committed_pmc_summary_is_consistent():
@@ -177,3 +186,54 @@ def test_particle_weight_allreduce_gloo_world2():
     np.testing.assert_allclose(got, w_all.tolist(), rtol=0, atol=0)
     assert abs(sum(got) - 1.0) < 1e-12
     assert res[0][1] == res[1][1] == neff_all
+
+
+# ----------------------------------------------------------------------------- RCCL unique id over gloo
+def _uid_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+
+    from slam2d.gmapping import _UniqueId, exchange_unique_id, unique_id_bytes
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    uid = _UniqueId()
+    if rank == 0:  # an ncclUniqueId-like id: family 2 then NULs, a port, an address, random tail bytes
+        raw = np.zeros(128, np.uint8)
+        raw[:16] = [2, 0, 0x9C, 0x41, 127, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0]
+        raw[100:128] = np.arange(1, 29, dtype=np.uint8)
+        C.memmove(C.addressof(uid), raw.tobytes(), 128)
+
+    def bcast(buf):  # the same callable bench.py hands RcclComm, on CPU tensors
+        t = torch.from_numpy(np.ascontiguousarray(buf))
+        dist.broadcast(t, 0)
+        return t.numpy()
+
+    got = exchange_unique_id(uid, world, rank, bcast)
+    out[rank] = unique_id_bytes(got).tobytes()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_unique_id_with_nul_bytes_gloo_world2():
+    """RcclComm's id broadcast (exchange_unique_id) carries all 128 bytes of an id that holds NULs
+    (a c_char field truncated it at the first NUL, so N > 1 could not start)."""
+    import torch.multiprocessing as mp
+
+    from slam2d.gmapping import _UniqueId, unique_id_bytes, unique_id_from_bytes
+
+    world = 2
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_uid_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    assert len(res[0]) == len(res[1]) == 128
+    assert res[0] == res[1]
+    assert res[1][:2] == b"\x02\x00" and res[1][-1] == 28
+    # round trip of the (de)serialisation itself
+    raw = np.random.default_rng(3).integers(0, 256, 128).astype(np.uint8)
+    raw[5] = 0
+    assert unique_id_bytes(unique_id_from_bytes(raw)).tobytes() == raw.tobytes()
+    with pytest.raises(Exception):
+        unique_id_from_bytes(raw[:1])
+    assert C.sizeof(_UniqueId) == 128

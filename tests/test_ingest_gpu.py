@@ -125,7 +125,7 @@ def test_step_ranges_matches_oracle_pipeline(gpu):
     fleet.set_update_factors(0.4, 0.9)
     fleet.set_thresholds(0.4, 0.9)
     fleet.set_laser(L)
-    oras = [O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=256) for _ in range(S)]
+    oras = [O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=0) for _ in range(S)]
     for o in oras:
         o.set_update_factors(0.4, 0.9)
         o.set_thresholds(0.4, 0.9)
@@ -163,7 +163,7 @@ def test_step_ranges_wide_scan_separate_ingest(gpu):
     fleet.set_update_factors(0.4, 0.9)
     fleet.set_thresholds(-1.0, -1.0)
     fleet.set_laser(L, unit_vectors=cs)
-    oras = [O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=256) for _ in range(S)]
+    oras = [O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=0) for _ in range(S)]
     for o in oras:
         o.set_update_factors(0.4, 0.9)
         o.set_thresholds(-1.0, -1.0)
@@ -311,7 +311,7 @@ def test_run_ranges_equals_per_step(gpu, monkeypatch, S, gate, pipeline):
     assert np.array_equal(da, db)
     assert np.array_equal(_bits(logs[0].cpu().numpy()), _bits(logs[1].cpu().numpy()))
     _maps_equal(fa, fb, S, LV)
-    o = O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=256)
+    o = O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=0)
     o.set_update_factors(0.4, 0.9)
     o.set_thresholds(*gate)
     cs = O.unit_vectors(N, float(AMIN), float(AINC))

@@ -8,7 +8,7 @@ from slam2d.hector import HectorFleet
 S = synth.make_streams(4, 3)
 for size, levels in ((1024, 1), (2048, 1), (1024, 3), (2048, 3), (512, 2)):
     f = HectorFleet(1, 0.05, size, (0.5, 0.5), levels, max_points=1081); f.set_update_factors(0.4, 0.9)
-    o = O.HectorOracle(0.05, size, (0.5, 0.5), levels, reduce_threads=256); o.set_update_factors(0.4, 0.9)
+    o = O.HectorOracle(0.05, size, (0.5, 0.5), levels, reduce_threads=0); o.set_update_factors(0.4, 0.9)
     pts = S.points[1, 0, :S.counts[1, 0]]
     pose = np.zeros(3, np.float32)
     f.update_by_scan(0, pts, pose); o.update_by_scan(pts, pose)

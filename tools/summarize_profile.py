@@ -39,6 +39,11 @@ def main():
     cfg = bench["config"]["config"]
     streams = next((bench["config"][k] for k in ("streams_per_gpu", "matches_per_gpu", "pairs_per_gpu", "particles_per_gpu")
                     if k in bench["config"]), None)
+    # the workload key bench.py matches on (Hector lines carry semantics and summation order)
+    wkey = {"config": cfg, "streams": streams}
+    for k, src in (("semantics", "semantics"), ("order", "reduction_order")):
+        if src in bench["config"]:
+            wkey[k] = bench["config"][src]
 
     dur = {}
     with open(stats) as f:
@@ -66,7 +71,7 @@ def main():
         lines.append(f"| {k} | {calls} | {avg / 1e3:.1f} | {fe if fe is not None else '-'} | "
                      f"{wr if wr is not None else '-'} | {tb if tb else '-'} | {gbs} |")
         if tb and k.startswith(("hs_", "kt_", "gm_", "pl_")):
-            entries.append({"kernel": k, "config": cfg, "streams": streams, "avg_ns": avg,
+            entries.append({"kernel": k, **wkey, "avg_ns": avg,
                             "fetch_kb": fe, "write_kb": wr, "traffic_bytes_per_launch": tb,
                             "source": f"profiles/{rnd}/{tag}_summary.md"})
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
@@ -78,8 +83,9 @@ def main():
             d = json.load(f)
     except (OSError, ValueError):
         d = {"entries": []}
-    keep = [e for e in d["entries"] if (e["kernel"], e["config"], e["streams"]) not in
-            {(n["kernel"], n["config"], n["streams"]) for n in entries}]
+    def ident(e):
+        return (e["kernel"], e["config"], e["streams"], e.get("semantics"), e.get("order"))
+    keep = [e for e in d["entries"] if ident(e) not in {ident(n) for n in entries}]
     d["entries"] = keep + entries
     with open(path, "w") as f:
         json.dump(d, f, indent=1)

@@ -315,26 +315,45 @@ __device__ __forceinline__ void point_accum(const PointFetch &pf, float cs, floa
 constexpr int SEQ_STRIDE = MATCH_THREADS + 4;
 constexpr int SEQ_WORDS = 9 * SEQ_STRIDE;
 
-// run + T[lane][0] + T[lane][1] + ... + T[lane][cnt - 1], left to right
+// run + T[lane][0] + T[lane][1] + ... + T[lane][cnt - 1], left to right.  The adds are one dependent
+// chain; the LDS reads of the next 16 terms are issued before the current 16 are added.
+#define S2D_ADD4(v) do { run = run + (v).x; run = run + (v).y; run = run + (v).z; run = run + (v).w; } while (0)
 __device__ __forceinline__ float seq_chain(const float *T, int lane, int cnt, float run)
 {
     const float4 *row = reinterpret_cast<const float4 *>(T + lane * SEQ_STRIDE);
     const int c4 = cnt >> 2;
     int i = 0;
-    for (; i + 3 < c4; i += 4) {
-        const float4 a = row[i], b = row[i + 1], c = row[i + 2], d = row[i + 3];
-        run = run + a.x; run = run + a.y; run = run + a.z; run = run + a.w;
-        run = run + b.x; run = run + b.y; run = run + b.z; run = run + b.w;
-        run = run + c.x; run = run + c.y; run = run + c.z; run = run + c.w;
-        run = run + d.x; run = run + d.y; run = run + d.z; run = run + d.w;
+    if (c4 >= 8) {
+        // two register sets of 16 terms, alternating: one set's reads are in flight while the other's
+        // adds run
+        float4 a0 = row[0], a1 = row[1], a2 = row[2], a3 = row[3];
+        float4 b0, b1, b2, b3;
+        for (i = 4; i + 7 < c4; i += 8) {
+            b0 = row[i]; b1 = row[i + 1]; b2 = row[i + 2]; b3 = row[i + 3];
+            __builtin_amdgcn_sched_barrier(0);  // keep the reads above the adds (the scheduler sinks them)
+            S2D_ADD4(a0); S2D_ADD4(a1); S2D_ADD4(a2); S2D_ADD4(a3);
+            a0 = row[i + 4]; a1 = row[i + 5]; a2 = row[i + 6]; a3 = row[i + 7];
+            __builtin_amdgcn_sched_barrier(0);
+            S2D_ADD4(b0); S2D_ADD4(b1); S2D_ADD4(b2); S2D_ADD4(b3);
+        }
+        S2D_ADD4(a0); S2D_ADD4(a1); S2D_ADD4(a2); S2D_ADD4(a3);
     }
     for (; i < c4; ++i) {
         const float4 a = row[i];
-        run = run + a.x; run = run + a.y; run = run + a.z; run = run + a.w;
+        S2D_ADD4(a);
     }
     const float *tail = T + lane * SEQ_STRIDE + (c4 << 2);
     for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];
     return run;
+}
+#undef S2D_ADD4
+
+// The wave that runs a workgroup's sequential sums and step tail.  Workgroups co-resident on one CU
+// tend to have block ids 256 apart (round-robin dispatch over the CUs), so the block id's bits 8-9 are
+// mixed in: their chain waves then sit on different SIMDs instead of sharing one.
+__device__ __forceinline__ int chain_wave()
+{
+    return (int)((blockIdx.x + (blockIdx.x >> 8)) & (MATCH_WAVES - 1));
 }
 
 // Workgroup barrier for LDS hand-offs only (waits for this wave's LDS operations, not for its global
@@ -356,7 +375,12 @@ __device__ __forceinline__ void seq_chunk(float *T, const float *t, bool has, bo
         for (int k = 0; k < 9; ++k) T[k * SEQ_STRIDE + tid] = t[k];
     }
     lds_barrier();
-    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);
+    if ((tid >> 6) == cw) {
+        // the chain is the workgroup's critical path (the other waves wait for it at the next barrier):
+        // it issues ahead of the co-resident workgroups' waves (s_setprio; back to 0 after the step tail)
+        __builtin_amdgcn_s_setprio(3);
+        if (lane < 9) run = seq_chain(T, lane, cnt, run);
+    }
 }
 
 // the 9 sums held by lanes 0..8 of the calling (chain) wave, in every lane of it
@@ -412,7 +436,7 @@ __device__ __forceinline__ void gn_step(const float *__restrict__ cells, const L
     const float sn = sdm_sinf(est[2]);
     float s[9];
     if constexpr (SEQ) {
-        const int cw = blockIdx.x & (MATCH_WAVES - 1);
+        const int cw = chain_wave();
         float run = 0.0f;
         for (int c0 = 0; c0 < n; c0 += MATCH_THREADS) {
             const int i = c0 + tid;
@@ -426,6 +450,7 @@ __device__ __forceinline__ void gn_step(const float *__restrict__ cells, const L
             seq_chunk(seqT, t, i < n, c0 == 0, min(MATCH_THREADS, n - c0), cw, run);
         }
         if ((tid >> 6) == cw && (tid & 63) < 9) red[parity][0][tid & 63] = run;
+        __builtin_amdgcn_s_setprio(0);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 9; ++k) s[k] = red[parity][0][k];
@@ -579,7 +604,7 @@ __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, con
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const int wave = tid >> 6;
-    const int cw = (int)(blockIdx.x & (MATCH_WAVES - 1));  // the chain / step-tail wave
+    const int cw = chain_wave();  // the chain / step-tail wave
     float run = 0.0f;                                       // SEQ: lane k < 9 of wave cw: sum of term k
     if constexpr (SEQ) {
         // chunk j = points j * 256 .. j * 256 + 255 = slot j of every thread, in point order
@@ -660,6 +685,7 @@ __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, con
             for (int k = 0; k < 9; ++k) sp[5 + k] = H[k];
             sp[14] = clamp;
         }
+        __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
     est[0] = sp[0];

@@ -375,9 +375,6 @@ __device__ __forceinline__ bool kt_group(unsigned long long gmask, bool ok, int 
     }
     // merge: 8 64-bit compare-and-swaps in flight per lane (a fresh word finishes in one), then the words that
     // already held data
-#if defined(KT_DIAG_NOMERGE)
-    if (nw > 0) return true;
-#endif
     for (int t0 = lane; t0 < nw; t0 += 64 * 8) {
         unsigned long long want[8], old[8];
 #pragma unroll
@@ -387,11 +384,7 @@ __device__ __forceinline__ bool kt_group(unsigned long long gmask, bool ok, int 
             old[u] = 0ull;
             if (want[u] != 0ull) {
                 const int r = t / ww, q = t - r * ww;
-#if defined(KT_DIAG_STORE)
-                gw[wbase + r * wsw + q] = want[u];
-#else
                 old[u] = atomicCAS(gw + wbase + r * wsw + q, 0ull, want[u]);
-#endif
             }
         }
 #pragma unroll
@@ -1219,7 +1212,6 @@ kt_select_kernel(KtGeom g, KtState *st, const double *__restrict__ resp, unsigne
     const int tid = threadIdx.x;
     const int nA = g.nang[pass];
     const int nxy = g.nxy;
-    const int np = nxy * nxy * nA;
     const double best = kt_dbl(S.best_bits);
     const double *r = resp + (size_t)m * g.max_poses;
     int *ti = tie_idx + (size_t)m * g.max_poses;
@@ -1444,7 +1436,7 @@ kt_fine_kernel(KtGeom g, KtPool P, KtState *st, const unsigned char *__restrict_
     __shared__ int s_gi;
     const int m = blockIdx.x;
     KtState &S = st[m];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
     const double cx = S.mean[0], cy = S.mean[1], ch = S.mean[2];  // rSearchCenter = coarse rMean
     const double gox = S.gox, goy = S.goy;
     const int q = S.query, npts = S.npts;

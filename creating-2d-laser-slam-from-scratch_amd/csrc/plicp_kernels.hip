@@ -27,6 +27,7 @@ namespace s2d {
 constexpr int PL_THREADS = 256;
 constexpr int PL_RPT_MAX = 8;                   // rays per thread: max_rays <= 2048
 constexpr int PL_MAX_RAYS = PL_THREADS * PL_RPT_MAX;
+static_assert(PL_MAX_RAYS == PL_MAX_SCAN_RAYS, "include/slam2d/plicp.h names the kernel's ray limit");
 constexpr int PL_MAX_IT = 64;
 #ifndef PL_CORE
 #define PL_CORE 4   // half-width of the core search around a point's own cell
@@ -62,7 +63,9 @@ __device__ __forceinline__ double pl_dist_to_segment(double ax, double ay, doubl
 // half-width) through a monotone double expression.  So each is first evaluated by a cheap float
 // approximation a with |a - exact| < PL_ATAN_EPS (measured by tools/check_fatan.c: 2.3e-7 worst case
 // over every non-negative float for pl_fatan, 4.1e-7 over 2e8 sampled double pairs for pl_fatan2, the
-// double -> float rounding of the arguments included; NaN / inf fall to the exact path): the integer the expression yields at a - eps and at a + eps brackets
+// double -> float rounding of the arguments included; its quick mode -- edge regions: |y/x| near 1,
+// tiny / huge ratios, arguments around FLT_MIN, near +-pi -- runs in tests/test_plicp_atan_cpu.py;
+// NaN / inf / zero / subnormal arguments fall to the exact path): the integer the expression yields at a - eps and at a + eps brackets
 // the exact one, and when the two agree that is the result -- the exact double evaluation (the
 // reference's value, sdm_atan / sdm_atan2) runs only when the bracket straddles an integer boundary
 // (about 2 eps / cell width, < 1e-3 of the evaluations).  Results are the exact path's, bit for bit.
@@ -115,7 +118,8 @@ __device__ __forceinline__ void pl_theta_cells(double wx, double wy, int n, doub
     auto sc = [&](double th) { return (int)((th - min_theta) / (max_theta - min_theta) * n); };
     auto cc = [&](double th) { return angle_inc > 0.0 ? (int)((th - min_theta) / angle_inc) : 0; };
     const float fx = (float)wx, fy = (float)wy;
-    if (fx != 0.0f && fy != 0.0f) {
+    // zero or subnormal magnitudes (their float rounding is not relative to 2^-24) take the exact path
+    if (fx != 0.0f && fy != 0.0f && fmaxf(fabsf(fx), fabsf(fy)) >= 1.17549435e-38f) {
         const double a = (double)pl_fatan2(fy, fx);
         // near +-pi the exact atan2 may sit on the other side of the cut: no bracket there
         if (fabs(a) <= SDM_PI - 4.0 * PL_ATAN_EPS) {

@@ -61,7 +61,9 @@ const char *pl_last_error(void);
 /* ScanMatchPLICP::InitParams values (plicp_odometry.cc:74-186) */
 void pl_default_params(pl_params *params);
 
-/* A context for up to max_pairs scan pairs of up to max_rays rays (max_rays <= 2048). */
+/* The device kernel's ray limit: 256 threads x 8 rays each (csrc/plicp_kernels.hip PL_MAX_RAYS). */
+#define PL_MAX_SCAN_RAYS 2048
+/* A context for up to max_pairs scan pairs of up to max_rays rays (max_rays <= PL_MAX_SCAN_RAYS). */
 int pl_create(pl_ctx **out, int max_pairs, int max_rays, const pl_params *params);
 int pl_destroy(pl_ctx *ctx);
 

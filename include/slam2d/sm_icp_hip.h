@@ -68,6 +68,12 @@ inline void slam2d_sm_icp(SmParams *input, SmResult *output)
         fail("laser_ref and laser_sens differ in nrays");
         return;
     }
+    if (n > PL_MAX_SCAN_RAYS) {
+        // not a once-only warning: every such scan fails (output->valid = 0), and says so
+        std::fprintf(stderr, "slam2d_sm_icp: %d rays; the device PL-ICP takes at most %d (PL_MAX_SCAN_RAYS)\n", n,
+                     PL_MAX_SCAN_RAYS);
+        return;
+    }
     for (int i = 0; i < n; ++i)
         if (ref->theta[i] != sens->theta[i]) {
             fail("laser_ref and laser_sens differ in theta");
@@ -86,7 +92,7 @@ inline void slam2d_sm_icp(SmParams *input, SmResult *output)
     p.max_iterations = input->max_iterations;
     p.use_point_to_line_distance = input->use_point_to_line_distance;
     p.outliers_remove_doubles = input->outliers_remove_doubles;
-    if (!sc.ctx && pl_create(&sc.ctx, 1, 2048, &p) != PL_OK) {
+    if (!sc.ctx && pl_create(&sc.ctx, 1, PL_MAX_SCAN_RAYS, &p) != PL_OK) {  // the largest context: any n fits
         fail(pl_last_error());
         return;
     }

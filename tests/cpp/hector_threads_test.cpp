@@ -65,7 +65,7 @@ int main(int argc, char **argv)
     std::vector<float> opose((size_t)K * 3);
     {
         ho_ctx *o = ho_create(0.05f, size, size, 0.5f, 0.5f, levels);
-        ho_set_mode(o, 256, 0);
+        ho_set_mode(o, 0, 0);  // the reference summation order: the library default
         ho_set_update_factors(o, 0.4f, 0.9f);
         ho_set_thresholds(o, -1.0f, -1.0f);
         std::vector<float> l(cells);

@@ -20,6 +20,14 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   lds6       same results   hs_update_kernel with 2.5 KB of unused LDS (7 -> 6 workgroups per CU: occupancy price)
   lds5       same results   hs_update_kernel with 10 KB of unused LDS (5 workgroups per CU)
   ktnoswar   WRONG RESULTS  kt_addscans_kernel dword render writes the kernel bytes without the byte max
+  ktnomerge  WRONG RESULTS  kt_build_kernel skips the 64-bit CAS merge of its tile into the match grid
+  ktstore    WRONG RESULTS  kt_build_kernel merges with plain stores instead of compare-and-swap
+  prio1      same results   hs_match_kernel's chain wave at s_setprio 3 while it extends the sequential sums
+  prio2      same results   prio1, and the step tail (solve, sin / cos) at s_setprio 3 too
+  seqnochain WRONG RESULTS  hs_match_kernel's sequential sum adds one term per chunk (prices the chain adds;
+                            the chunk hand-offs and barriers stay)
+  seq4acc    WRONG RESULTS  hs_match_kernel's sequential sum in 4 interleaved accumulators (same instruction
+                            count, a quarter of the dependency depth: latency vs issue)
 """
 import os
 import shutil
@@ -53,6 +61,26 @@ PATCHES = {
               "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points)) + 2560;\n    const bool single")],
     "lds5": [("hector_capi.hip", "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));\n    const bool single",
               "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points)) + 10240;\n    const bool single")],
+    "ktnomerge": [("karto_kernels.hip", "    for (int t0 = lane; t0 < nw; t0 += 64 * 8) {\n        unsigned long long want[8], old[8];",
+                   "    if (nw > 0) return true;\n    for (int t0 = lane; t0 < nw; t0 += 64 * 8) {\n        unsigned long long want[8], old[8];")],
+    "ktstore": [("karto_kernels.hip", "                old[u] = atomicCAS(gw + wbase + r * wsw + q, 0ull, want[u]);",
+                 "                gw[wbase + r * wsw + q] = want[u];")],
+    "prio1": [(K, "    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);",
+               "    if ((tid >> 6) == cw) {\n        __builtin_amdgcn_s_setprio(3);\n        if (lane < 9) run = seq_chain(T, lane, cnt, run);\n"
+               "        __builtin_amdgcn_s_setprio(0);\n    }")],
+    "prio2": [(K, "    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);",
+               "    if ((tid >> 6) == cw) {\n        __builtin_amdgcn_s_setprio(3);\n        if (lane < 9) run = seq_chain(T, lane, cnt, run);\n"
+               "    }"),
+              (K, "            sp[14] = clamp;\n        }\n    }\n    __syncthreads();",
+               "            sp[14] = clamp;\n        }\n        __builtin_amdgcn_s_setprio(0);\n    }\n    __syncthreads();")],
+    "seqnochain": [(K, "    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);",
+                    "    if ((tid >> 6) == cw && lane < 9) run = run + T[lane * SEQ_STRIDE];")],
+    "seq4acc": [(K, "#define S2D_ADD4(v) do { run = run + (v).x; run = run + (v).y; run = run + (v).z; run = run + (v).w; } while (0)",
+                 "#define S2D_ADD4(v) do { run = run + (v).x; r1 = r1 + (v).y; r2 = r2 + (v).z; r3 = r3 + (v).w; } while (0)"),
+                (K, "    const float4 *row = reinterpret_cast<const float4 *>(T + lane * SEQ_STRIDE);\n    const int c4 = cnt >> 2;",
+                 "    const float4 *row = reinterpret_cast<const float4 *>(T + lane * SEQ_STRIDE);\n    const int c4 = cnt >> 2;\n    float r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;"),
+                (K, "    for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];\n    return run;",
+                 "    for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];\n    return run + (r1 + (r2 + r3));")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

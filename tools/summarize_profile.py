@@ -41,9 +41,9 @@ def main():
                     if k in bench["config"]), None)
     # the workload key bench.py matches on (Hector lines carry semantics and summation order)
     wkey = {"config": cfg, "streams": streams}
-    for k, src in (("semantics", "semantics"), ("order", "reduction_order")):
-        if src in bench["config"]:
-            wkey[k] = bench["config"][src]
+    for k, field in (("semantics", "semantics"), ("order", "reduction_order")):
+        if field in bench["config"]:
+            wkey[k] = bench["config"][field]
 
     dur = {}
     with open(stats) as f:

@@ -254,7 +254,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
     __syncthreads();
     // ---- rays (:185-214), computed by gm_score_kernel
     int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
-    for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
+    for (int b0 = __builtin_amdgcn_readfirstlane(tid & ~63); b0 < n; b0 += GM_THREADS) {
         const int b = b0 + (tid & 63);
         unsigned r = GM_RAY_INVALID;
         int gx0 = x0, gy0 = y0, gx1 = x0, gy1 = y0;
@@ -303,7 +303,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
         // the flag of this parity was last read two tiles ago, with barriers in between
         if (tid == 0) s_anyf[it & 1] = 0;
         gm_lds_barrier();
-        for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
+        for (int b0 = __builtin_amdgcn_readfirstlane(tid & ~63); b0 < n; b0 += GM_THREADS) {
             const int4 gb = gbox[b0 >> 6];
             const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
             const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
@@ -366,7 +366,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
         any_tile_marks = false;
         unsigned *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
         // acc: the first hitting beam of a cell sums every hit of that cell in beam order (:236-240)
-        for (int b0 = tid & ~63; b0 < n; b0 += GM_THREADS) {
+        for (int b0 = __builtin_amdgcn_readfirstlane(tid & ~63); b0 < n; b0 += GM_THREADS) {
             const int4 gb = gbox[b0 >> 6];
             const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
             const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);

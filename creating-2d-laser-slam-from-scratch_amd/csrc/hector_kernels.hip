@@ -1676,7 +1676,10 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
     unsigned long long L = 0, R = 0;
     const float2 *pts = lvl == 0 ? xy + (size_t)local * xy_stride : mc + (size_t)s * mc_stride;
-    for (int b0 = tid & ~63; (b0 & ~255) < n; b0 += UPD_THREADS) {   // wave-uniform trip count
+    // the wave's first beam in a scalar register: the fan-group loops and the ray-register selects below
+    // then compile to scalar control (tid & ~63 in a VGPR made them divergent loops with exec-mask code)
+    const int wave_beam0 = __builtin_amdgcn_readfirstlane(tid & ~63);
+    for (int b0 = wave_beam0; (b0 & ~255) < n; b0 += UPD_THREADS) {   // wave-uniform trip count
         const int b = fan_beam(b0, lane);
         unsigned r = RAY_INVALID;
         if (b < n) {
@@ -1761,8 +1764,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         const int X0 = tx * TILE, Y0 = ty * UPD_TH;
         const int X1 = X0 + TILE, Y1 = Y0 + UPD_TH;
         if (i < my_tiles) {
-            bool any = false;
-            for (int b0 = tid & ~63; (b0 & ~255) < n; b0 += UPD_THREADS) {
+            unsigned anyv = 0u;  // a VGPR flag: no exec-mask merging of a divergent bool
+            for (int b0 = wave_beam0; (b0 & ~255) < n; b0 += UPD_THREADS) {
                 // wave-uniform fan-group test (scalar)
                 const int4 gb = gbox[b0 >> 6];
                 const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
@@ -1782,7 +1785,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     const int c = (y1 - Y0) * TILE + (x1 - X0);
                     atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
                     atomicOr(&hitb[c >> 5], 1u << (c & 31));
-                    any = true;
+                    anyv = 1u;
                 }
                 const RayWalk w = ray_walk(x0, y0, x1, y1);
                 // the tile in (major, minor) order, selected before ONE clip (lanes of a fan that straddles
@@ -1793,7 +1796,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 if (!walk_range(w, A0, A1, B0, B1, lo_i, hi_i)) continue;
                 if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
                 if (lo_i > hi_i) continue;
-                any = true;
+                anyv = 1u;
                 const int scnt = hi_i - lo_i + 1;     // free steps of this beam inside the tile
                 const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
                 const int q = (int)udiv_small(num, (unsigned)w.da);
@@ -1828,7 +1831,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
 #undef S2D_WSTEP
                 if (k < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
             }
-            if (__ballot(any) && lane == 0) s_any[buf] = (unsigned)(i + 1);
+            if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);
         }
         if (pend_tl) {
             // apply the previous tile: log-odds of every marked cell, both planes written (see below);

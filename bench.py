@@ -46,6 +46,22 @@ KERNELS = ("match", "bin", "update")
 PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")  # written by tools/summarize_profile.py
 
 
+def kernel_source_id() -> str:
+    """16 hex digits of sha256 over the Hector kernel sources: a PMC summary is attached to a bench line
+    only when it was taken with the same kernels (tools/summarize_profile.py records it)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = os.path.join(PKG, "csrc")
+    for name in ("hector_kernels.hip", "hector_capi.hip", "hector_internal.h", "detmath.h"):
+        try:
+            with open(os.path.join(csrc, name), "rb") as f:
+                h.update(f.read())
+        except OSError:
+            return ""
+    return h.hexdigest()[:16]
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -743,7 +759,8 @@ def main():
     if args.order == "tree":
         fleet.set_reduction_order(HectorFleet.ORDER_TREE256)
     order = fleet.reduction_order()
-    workload = {"config": args.config, "streams": B, "semantics": args.semantics, "order": order}
+    workload = {"config": args.config, "streams": B, "semantics": args.semantics, "order": order,
+                "kernel_src": kernel_source_id()}
     hs = torch.cuda.current_stream(dev).cuda_stream
     # pose log: every 64th stream and the last one (the top of the update lists and of the HBM range)
     log_streams = sorted(set(range(0, B, 64)) | {B - 1})
@@ -894,7 +911,7 @@ def main():
                                         if os.environ.get("SLAM2D_PIPELINE", "0") not in ("", "0") else ""))
                                     if pipelined else "one batch call per step"),
                           "parallelism": f"replicas x{world}", "semantics": args.semantics,
-                          "reduction_order": order,
+                          "reduction_order": order, "kernel_src": workload["kernel_src"],
                           "map_updates_per_scan": round(ctr["updates"] / max(B * K, 1), 4)},
                "roofline": roof, "cpu_baseline": cpu, "pose_vs_ref": pose}
         if cpu:

@@ -236,8 +236,8 @@ __device__ __forceinline__ void point_fetch(const float *__restrict__ lvl_words,
         const unsigned ux = (unsigned)ix, uy = (unsigned)iy;  // >= 0 by the bounds check
         const float *r0 = lvl_words + cell_word(g, (int)ux, (int)uy);
         const float *r1 = lvl_words + cell_word(g, (int)ux, (int)(uy + 1));
-        if ((ux & (TILE - 1)) != TILE - 1) {
-            // (ix, ix + 1) are adjacent words of one tile row: one 8-byte (4-byte aligned) gather per row
+        if ((ux & (CELL_BLK - 1)) != CELL_BLK - 1) {
+            // (ix, ix + 1) are adjacent words of one block row: one 8-byte (4-byte aligned) gather per row
             float2 a, b;
             __builtin_memcpy(&a, r0, 8);
             __builtin_memcpy(&b, r1, 8);
@@ -563,7 +563,7 @@ __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, con
                     const unsigned ux = (unsigned)ix, uy = (unsigned)iy;
                     const float *r0 = cells + cell_word(g, (int)ux, (int)uy);
                     const float *r1 = cells + cell_word(g, (int)ux, (int)(uy + 1));
-                    if ((ux & (TILE - 1)) != TILE - 1) {
+                    if ((ux & (CELL_BLK - 1)) != CELL_BLK - 1) {  // (ix, ix + 1) adjacent in a block row
                         float2 a, b;
                         __builtin_memcpy(&a, r0, 8);
                         __builtin_memcpy(&b, r1, 8);
@@ -1387,7 +1387,7 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
 #pragma unroll
             for (int row = 0; row < TILE_H; ++row) {
                 const int gy = Y0 + row;
-                if (((rowmask >> row) & 1u) && colok && gy < g.sy) cl[row] = tl[row * TILE + lane];
+                if (((rowmask >> row) & 1u) && colok && gy < g.sy) cl[row] = tl[tile_cell(lane, row)];
             }
             S2D_STAMP(tb);
             bool any = false;
@@ -1484,8 +1484,8 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
                         if (l < 50.0f) l = l + lo;  // updateSetOccupied (:108-114)
                         upd = mark_occ;
                     }
-                    tl[row * TILE + lane] = l;
-                    tu[row * TILE + lane] = upd;
+                    tl[tile_cell(lane, row)] = l;
+                    tu[tile_cell(lane, row)] = upd;
                     ++touched;
                 }
 #pragma unroll
@@ -1568,12 +1568,13 @@ __device__ __forceinline__ float apply_cell(float l, unsigned odd, unsigned hit,
     return l;
 }
 
-// word offset of LDS-tile row `row` inside the level's tiled storage, relative to the LDS tile's
-// first storage tile (rows past TILE_H continue in the storage tile below)
-__device__ __forceinline__ int upd_off(int row, int tiles_x)
+// word offset of the quad at (c4, row) of the LDS tile (c4 % 4 == 0: 4 contiguous cells of a block row)
+// inside the level's tiled storage, relative to the LDS tile's first storage tile (rows past TILE_H
+// continue in the storage tile below)
+__device__ __forceinline__ int upd_off(int row, int c4, int tiles_x)
 {
-    if constexpr (UPD_TH == TILE_H) return row * TILE;
-    return (row / TILE_H) * tiles_x * TILE_BLOCK_WORDS + (row % TILE_H) * TILE;
+    if constexpr (UPD_TH == TILE_H) return tile_cell(c4, row);
+    return (row / TILE_H) * tiles_x * TILE_BLOCK_WORDS + tile_cell(c4, row % TILE_H);
 }
 
 constexpr int UPD_HIT_WORDS = UPD_TH * (TILE / 32);                  // one hit bit per tile cell
@@ -1846,7 +1847,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 const unsigned mb = qb[j];
                 if (!(mb & 15u)) continue;
                 const int qi = tid + j * UPD_THREADS;
-                const int o = upd_off(qi >> 4, g.tiles_x) + ((qi & 15) << 2);
+                const int o = upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
@@ -1888,7 +1889,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                                         ((unsigned)(m.z != W_NONE) << 2) | ((unsigned)(m.w != W_NONE) << 3);
                     const unsigned od = (m.x & 1u) | ((m.y & 1u) << 1) | ((m.z & 1u) << 2) | ((m.w & 1u) << 3);
                     qb[j] = mk | ((od & mk) << 4) | ((h & mk) << 8);
-                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(&pend_tl[upd_off(row, g.tiles_x) + c4]);
+                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(&pend_tl[upd_off(row, c4, g.tiles_x)]);
                     // restore: the quad's event words (read by this thread only) and, by the first of
                     // the 8 lanes sharing it, the hit-bit word (its readers are this wave's lanes, whose
                     // read above precedes this write)

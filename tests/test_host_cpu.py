@@ -99,7 +99,7 @@ def test_pmc_traffic_lookup(tmp_path, monkeypatch):
     w = {"config": "northstar", "streams": 1024, "semantics": "forced", "order": 0}
     got, why = bench.pmc_traffic("hs_update_kernel", w, 1100.0)
     assert got["traffic_bytes_per_launch"] == 123 and why == "x"
-    for k, v in (("config", "c2"), ("streams", 2048), ("semantics", "reference"), ("order", 256)):
+    for k, v in (("config", "c2"), ("streams", 2048), ("semantics", "reference"), ("order", 256), ("kernel_src", "x")):
         assert bench.pmc_traffic("hs_update_kernel", {**w, k: v}, 1000.0)[0] is None, k
     got, why = bench.pmc_traffic("hs_update_kernel", w, 2000.0)   # another build: refused
     assert got is None and "another build" in why

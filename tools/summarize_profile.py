@@ -41,7 +41,7 @@ def main():
                     if k in bench["config"]), None)
     # the workload key bench.py matches on (Hector lines carry semantics and summation order)
     wkey = {"config": cfg, "streams": streams}
-    for k, field in (("semantics", "semantics"), ("order", "reduction_order")):
+    for k, field in (("semantics", "semantics"), ("order", "reduction_order"), ("kernel_src", "kernel_src")):
         if field in bench["config"]:
             wkey[k] = bench["config"][field]
 
@@ -84,7 +84,7 @@ def main():
     except (OSError, ValueError):
         d = {"entries": []}
     def ident(e):
-        return (e["kernel"], e["config"], e["streams"], e.get("semantics"), e.get("order"))
+        return (e["kernel"], e["config"], e["streams"], e.get("semantics"), e.get("order"), e.get("kernel_src"))
     keep = [e for e in d["entries"] if ident(e) not in {ident(n) for n in entries}]
     d["entries"] = keep + entries
     with open(path, "w") as f:

@@ -959,10 +959,13 @@ __device__ __forceinline__ unsigned make_ray(const LevelGeom &g, const RayFrame 
 // correction step each way -- ~8 instructions instead of the ~25 of the integer division sequence.
 // Exact whenever the quotient is < 2^16, which covers every step index (<= 32767) it is compared
 // with; a larger quotient stays > 2^15 and only ever means "beyond the walk".
+// The products here use the full-rate 24-bit multiply (v_mul_u32_u24; v_mul_lo_u32 is quarter rate): q * d
+// is exact while q < 2^24 (d < 2^16, so the product < 2^32); a larger q -- a true quotient of at least
+// ~2^24 -- stays within +-1 of it, still "beyond the walk".
 __device__ __forceinline__ unsigned udiv_rcp(unsigned n, unsigned d, float rcp_d)  // rcp_d = rcp((float)d)
 {
     unsigned q = (unsigned)((float)n * rcp_d);
-    int r = (int)(n - q * d);
+    int r = (int)(n - __umul24(q, d));
     if (r < 0) {
         --q;
         r += (int)d;
@@ -974,7 +977,7 @@ __device__ __forceinline__ unsigned udiv_small(unsigned n, unsigned d)
 {
 #if S2D_FAST_UDIV
     unsigned q = (unsigned)((float)n * __builtin_amdgcn_rcpf((float)d));
-    int r = (int)(n - q * d);
+    int r = (int)(n - __umul24(q, d));  // callers: quotient < 2^16 (see udiv_rcp)
     if (r < 0) {
         --q;
         r += (int)d;
@@ -1023,10 +1026,10 @@ __device__ __forceinline__ bool walk_range(const RayWalk &w, int A0, int A1, int
     const int qlo = w.sb > 0 ? e0 : -e1, qhi = w.sb > 0 ? e1 : -e0;
     const unsigned dbs = w.db ? (unsigned)w.db : 1u;
     const float rdb = __builtin_amdgcn_rcpf((float)dbs);
-    // numerator > 0 when qlo > 0: qlo * da - e0 >= da - da / 2
-    const int n1 = qlo > 0 ? qlo * w.da - w.e0 + w.db - 1 : 0;
+    // numerator > 0 when qlo > 0: qlo * da - e0 >= da - da / 2   (|qlo|, |qhi|, da < 2^15: 24-bit products)
+    const int n1 = qlo > 0 ? __mul24(qlo, w.da) - w.e0 + w.db - 1 : 0;
     // numerator >= 0 when qhi >= 0: (qhi + 1) * da - e0 - 1 >= da - da / 2 - 1
-    const int n2 = qhi >= 0 ? (qhi + 1) * w.da - w.e0 - 1 : 0;
+    const int n2 = qhi >= 0 ? __mul24(qhi + 1, w.da) - w.e0 - 1 : 0;
     const int t = (int)udiv_rcp((unsigned)n1, dbs, rdb), t2 = (int)udiv_rcp((unsigned)n2, dbs, rdb);
     if (w.db != 0) {
         if (qlo > 0 && t > lo) lo = t;
@@ -1799,14 +1802,16 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 if (lo_i > hi_i) continue;
                 anyv = 1u;
                 const int scnt = hi_i - lo_i + 1;     // free steps of this beam inside the tile
-                const unsigned num = (unsigned)w.e0 + (unsigned)lo_i * (unsigned)w.db;
+                // (lo_i, db, q, da < 2^15 and the tile offsets < 2^7: 24-bit multiplies throughout)
+                const unsigned num = (unsigned)w.e0 + __umul24((unsigned)lo_i, (unsigned)w.db);
                 const int q = (int)udiv_small(num, (unsigned)w.da);
-                const int err = (int)(num - (unsigned)q * (unsigned)w.da);
+                const int err = (int)(num - __umul24((unsigned)q, (unsigned)w.da));
                 const unsigned ev = 2u * (unsigned)b + 1u;
                 // LDS index of step lo_i and its increments along the major / minor axis
                 const int la = w.x_major ? 1 : UPD_STRIDE;
                 const int lb = w.x_major ? UPD_STRIDE : 1;
-                const int li = (w.a0 + w.sa * lo_i - A0) * la + (w.b0 + w.sb * q - B0) * lb;
+                const int ia = w.a0 + (w.sa > 0 ? lo_i : -lo_i) - A0, ib = w.b0 + (w.sb > 0 ? q : -q) - B0;
+                const int li = __mul24(ia, la) + __mul24(ib, lb);
                 // incremental walk on byte offsets into the mark array, f = da - 1 - error_b in [0, da):
                 // the minor axis steps when f < db -- a subtract with borrow and two selects per step,
                 // four steps per trip

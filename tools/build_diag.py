@@ -24,6 +24,12 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   ktstore    WRONG RESULTS  kt_build_kernel merges with plain stores instead of compare-and-swap
   prio1      same results   hs_match_kernel's chain wave at s_setprio 3 while it extends the sequential sums
   prio2      same results   prio1, and the step tail (solve, sin / cos) at s_setprio 3 too
+  phase1     same results   hs_match_kernel: workgroups with block id bit 8 set start ~3.6 us late (s_sleep): are
+                            the co-resident workgroups' GN steps in lockstep?
+  phase2     same results   the same, ~7 us
+  noorigin   WRONG RESULTS  hs_update_kernel skips every ray's first 8 free steps (prices the dense cells around
+                            the scan origin, where the lanes' atomics hit the same words)
+  nohitbit   WRONG RESULTS  hs_update_kernel sets no hit bits (prices the end cells' atomicOr on shared words)
   seqnochain WRONG RESULTS  hs_match_kernel's sequential sum adds one term per chunk (prices the chain adds;
                             the chunk hand-offs and barriers stay)
   seq4acc    WRONG RESULTS  hs_match_kernel's sequential sum in 4 interleaved accumulators (same instruction
@@ -73,6 +79,14 @@ PATCHES = {
                "    }"),
               (K, "            sp[14] = clamp;\n        }\n    }\n    __syncthreads();",
                "            sp[14] = clamp;\n        }\n        __builtin_amdgcn_s_setprio(0);\n    }\n    __syncthreads();")],
+    "phase1": [(K, "    load_exptab();\n    __syncthreads();\n    const float *scells",
+                "    if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_sleep(127);\n    load_exptab();\n    __syncthreads();\n    const float *scells")],
+    "phase2": [(K, "    load_exptab();\n    __syncthreads();\n    const float *scells",
+                "    if ((blockIdx.x >> 8) & 1) { __builtin_amdgcn_s_sleep(127); __builtin_amdgcn_s_sleep(127); }\n"
+                "    load_exptab();\n    __syncthreads();\n    const float *scells")],
+    "noorigin": [(K, "                if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)\n                if (lo_i > hi_i) continue;",
+                  "                if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)\n                if (lo_i < 8) lo_i = 8;\n                if (lo_i > hi_i) continue;")],
+    "nohitbit": [(K, "                    atomicOr(&hitb[c >> 5], 1u << (c & 31));\n", "                    (void)c;\n")],
     "seqnochain": [(K, "    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);",
                     "    if ((tid >> 6) == cw && lane < 9) run = run + T[lane * SEQ_STRIDE];")],
     "seq4acc": [(K, "#define S2D_ADD4(v) do { run = run + (v).x; run = run + (v).y; run = run + (v).z; run = run + (v).w; } while (0)",

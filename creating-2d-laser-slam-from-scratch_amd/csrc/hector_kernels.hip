@@ -1538,7 +1538,12 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
 #ifndef S2D_UPD_STRIDE
 #define S2D_UPD_STRIDE 68
 #endif
-constexpr int UPD_STRIDE = S2D_UPD_STRIDE;            // LDS words per tile row (16-B rows, no 64-stride conflicts)
+// LDS words per tile row: 16-B rows (the apply reads and restores a quad's marks as one uint4) whose
+// stride is not a multiple of 32 banks.  (67, odd, spreads a column of cells over all 32 banks of an
+// atomic's lane group instead of 8, but the raster's conflicts are mostly lanes on the SAME word, which
+// no stride changes -- tools/lds_sim.py: 2 % fewer raster LDS cycles -- and the unaligned quads cost the
+// apply more: measured 0.005 ms slower.)
+constexpr int UPD_STRIDE = S2D_UPD_STRIDE;
 #ifndef S2D_UPD_TH
 #define S2D_UPD_TH 32
 #endif
@@ -1594,9 +1599,13 @@ __device__ __forceinline__ int lane_rank(unsigned long long m)  // set lanes bel
 }
 
 // Fan groups: the 64 beams a wave rasters together.  S2D_FAN_STRIDE 1 (default): 64 consecutive beams
-// (a 16 deg fan at 0.25 deg); 4: beams 256 G + 4 k + w for wave w of super-group G (a 64 deg fan,
-// 1 deg apart), so that near the scan origin the lanes of one LDS atomic address distinct cells --
-// measured slower (0.82 vs 0.78 ms): the wider fans lose more to culling than the conflicts cost.
+// (a 16 deg fan at 0.25 deg), lane l walking beam 2 (l % 32) + l / 32: each 32-lane half of an LDS
+// atomic (its banking group) spans the whole fan, and with the odd lanes walking backwards (see the
+// raster) the forward lanes of a half are 1 deg apart instead of 0.25 -- near the scan origin fewer
+// lanes land on one word (tools/lds_sim.py: 0.66 vs 0.75 of the consecutive order's raster LDS cycles).
+// 4: beams 256 G + 4 k + w for wave w of super-group G (a 64 deg fan, 1 deg apart), so that near the
+// scan origin the lanes of one LDS atomic address distinct cells -- measured slower (round 2, 0.82 vs
+// 0.78 ms): the wider fans lose more to culling than the conflicts cost.
 #ifndef S2D_FAN_STRIDE
 #define S2D_FAN_STRIDE 1
 #endif
@@ -1605,7 +1614,7 @@ __device__ __forceinline__ int fan_beam(int b0, int lane)  // b0 = 256 G + 64 w
 #if S2D_FAN_STRIDE == 4
     return (b0 & ~255) + 4 * lane + ((b0 >> 6) & 3);
 #else
-    return b0 + lane;
+    return b0 + 2 * (lane & 31) + (lane >> 5);
 #endif
 }
 __host__ __device__ constexpr int fan_groups(int max_points) { return ((max_points + 255) / 256) * 4; }
@@ -1802,22 +1811,29 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 if (lo_i > hi_i) continue;
                 anyv = 1u;
                 const int scnt = hi_i - lo_i + 1;     // free steps of this beam inside the tile
-                // (lo_i, db, q, da < 2^15 and the tile offsets < 2^7: 24-bit multiplies throughout)
-                const unsigned num = (unsigned)w.e0 + __umul24((unsigned)lo_i, (unsigned)w.db);
+                // Odd lanes walk their segment backwards, from hi_i down to lo_i (the same cells; the step
+                // below is its own inverse in g = da - 1 - f): at one instruction neighbouring beams then sit
+                // at different radii, so near the scan origin half as many lanes hit one LDS word (the
+                // atomics to one address serialise).
+                const bool bwd = (lane & 1) != 0;
+                const int s0 = bwd ? hi_i : lo_i;
+                // (s0, db, q, da < 2^15 and the tile offsets < 2^7: 24-bit multiplies throughout)
+                const unsigned num = (unsigned)w.e0 + __umul24((unsigned)s0, (unsigned)w.db);
                 const int q = (int)udiv_small(num, (unsigned)w.da);
                 const int err = (int)(num - __umul24((unsigned)q, (unsigned)w.da));
                 const unsigned ev = 2u * (unsigned)b + 1u;
-                // LDS index of step lo_i and its increments along the major / minor axis
+                // LDS index of step s0 and its increments along the major / minor axis
                 const int la = w.x_major ? 1 : UPD_STRIDE;
                 const int lb = w.x_major ? UPD_STRIDE : 1;
-                const int ia = w.a0 + (w.sa > 0 ? lo_i : -lo_i) - A0, ib = w.b0 + (w.sb > 0 ? q : -q) - B0;
+                const int ia = w.a0 + (w.sa > 0 ? s0 : -s0) - A0, ib = w.b0 + (w.sb > 0 ? q : -q) - B0;
                 const int li = __mul24(ia, la) + __mul24(ib, lb);
-                // incremental walk on byte offsets into the mark array, f = da - 1 - error_b in [0, da):
-                // the minor axis steps when f < db -- a subtract with borrow and two selects per step,
-                // four steps per trip
-                const int dab = w.sa * la * 4, dab2 = dab + w.sb * lb * 4;
+                // incremental walk on byte offsets into the mark array, f = da - 1 - error_b in [0, da)
+                // (backwards: g = error_b): the minor axis steps when f < db -- a subtract with borrow and
+                // two selects per step, four steps per trip
+                const int dab1 = w.sa * la * 4, dab21 = dab1 + w.sb * lb * 4;
+                const int dab = bwd ? -dab1 : dab1, dab2 = bwd ? -dab21 : dab21;
                 const int da_ = w.da, db_ = w.db;
-                int f = da_ - 1 - err;
+                int f = bwd ? err : da_ - 1 - err;
                 char *pm = reinterpret_cast<char *>(marks) + li * 4;
                 int k = 0;
 #define S2D_WSTEP                                                                 \

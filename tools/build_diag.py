@@ -29,7 +29,10 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   phase2     same results   the same, ~7 us
   noorigin   WRONG RESULTS  hs_update_kernel skips every ray's first 8 free steps (prices the dense cells around
                             the scan origin, where the lanes' atomics hit the same words)
-  nohitbit   WRONG RESULTS  hs_update_kernel sets no hit bits (prices the end cells' atomicOr on shared words)
+  nohitbit   WRONG RESULTS  hs_update_kernel sets no hit bits (prices the end cells' atomicOr on shared words).
+                            CONFOUNDED: with no occupied cells the match drifts, so the rays and the tiles they
+                            cover change; a hit-bit word map with <= 4 cells per word timed the same as the
+                            32-cell half-row words (round 3), i.e. the atomicOr is not what this variant saves
   seqnochain WRONG RESULTS  hs_match_kernel's sequential sum adds one term per chunk (prices the chain adds;
                             the chunk hand-offs and barriers stay)
   seq4acc    WRONG RESULTS  hs_match_kernel's sequential sum in 4 interleaved accumulators (same instruction

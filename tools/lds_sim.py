@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Offline model of hs_update_kernel's raster LDS traffic: which mark words the lanes of one wave hit
+with each free-mark atomic, and the LDS cycles that costs under the gfx950 banking rule for a 32-bit
+LDS write / atomic (2 groups of 32 lanes, bank = word mod 32, one cycle per distinct lane on the
+busiest bank: atomics do not broadcast).  Used to compare mark-array layouts and lane schedules
+(stride, backward odd lanes, beam-to-lane order) before spending GPU time; not a test.
+
+  python tools/lds_sim.py [--streams 2] [--scan 5]
+"""
+import argparse
+import math
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "creating-2d-laser-slam-from-scratch_amd", "python"))
+from slam2d import synth  # noqa: E402
+
+TILE, TH = 64, 32
+
+
+def rays_for(points, pose_cell, theta, level):
+    f = 1.0 / (1 << level)
+    cs, sn = math.cos(theta), math.sin(theta)
+    mx, my = pose_cell[0] * f, pose_cell[1] * f
+    x0, y0 = int(mx + 0.5), int(my + 0.5)
+    p = points * f
+    ex = mx + (cs * p[:, 0] - sn * p[:, 1]) + 0.5
+    ey = my + (sn * p[:, 0] + cs * p[:, 1]) + 0.5
+    x1, y1 = ex.astype(np.int64), ey.astype(np.int64)
+    return x0, y0, x1, y1
+
+
+def walk(x0, y0, x1, y1):
+    dx, dy = x1 - x0, y1 - y0
+    adx, ady = abs(dx), abs(dy)
+    sx, sy = (1 if dx > 0 else -1), (1 if dy > 0 else -1)
+    if adx >= ady:
+        return dict(xm=True, a0=x0, b0=y0, sa=sx, sb=sy, da=adx, db=ady, e0=adx // 2)
+    return dict(xm=False, a0=y0, b0=x0, sa=sy, sb=sx, da=ady, db=adx, e0=ady // 2)
+
+
+def cells_in_tile(w, X0, Y0):
+    """free steps 0..da-1 of the walk inside the tile: list of (step, lx, ly)."""
+    i = np.arange(w["da"])
+    q = (w["e0"] + i * w["db"]) // max(w["da"], 1)
+    a = w["a0"] + w["sa"] * i
+    b = w["b0"] + w["sb"] * q
+    x, y = (a, b) if w["xm"] else (b, a)
+    m = (x >= X0) & (x < X0 + TILE) & (y >= Y0) & (y < Y0 + TH)
+    return x[m] - X0, y[m] - Y0
+
+
+ORDERS = {
+    "id": lambda l: l,                                  # lane l: beam l of the fan
+    "split": lambda l: 2 * (l & 31) + (l >> 5),         # lane group g (32 lanes): beams of parity g
+}
+
+
+def wave_cycles(fan_cells, stride, bwd_odd, order="id"):
+    """fan_cells[b] = (lx, ly) arrays in walk order for beam b of the fan; lane l walks beam ORDERS[order](l)."""
+    lanes_cells = [fan_cells[ORDERS[order](l)] for l in range(64)]
+    n = [len(c[0]) for c in lanes_cells]
+    addrs = []
+    for l in range(64):
+        lx, ly = lanes_cells[l]
+        a = ly * stride + lx
+        if bwd_odd and (l & 1):
+            a = a[::-1]
+        addrs.append(a)
+    # instruction schedule: 4-step trips, then one 2-step trip, then the last single step
+    sched = []
+    j = 0
+    while any(4 * j + 3 < k for k in n):
+        for u in range(4):
+            sched.append([(l, 4 * j + u) for l in range(64) if 4 * j + 3 < n[l]])
+        j += 1
+    k4 = [4 * (k // 4) for k in n]
+    if any(k - k4[l] >= 2 for l, k in enumerate(n)):
+        for u in range(2):
+            sched.append([(l, k4[l] + u) for l in range(64) if n[l] - k4[l] >= 2])
+    k2 = [k4[l] + (2 if n[l] - k4[l] >= 2 else 0) for l in range(64)]
+    if any(n[l] - k2[l] == 1 for l in range(64)):
+        sched.append([(l, k2[l]) for l in range(64) if n[l] - k2[l] == 1])
+    cyc = ideal = same = 0
+    for ins in sched:
+        for g in (0, 1):
+            act = [addrs[l][s] for l, s in ins if (l >> 5) == g]
+            if not act:
+                continue
+            act = np.asarray(act)
+            banks = np.bincount(act % 32, minlength=32)
+            cyc += int(banks.max())
+            ideal += 1
+            _, cnt = np.unique(act, return_counts=True)
+            same += int(cnt.max() - 1)
+    return cyc, ideal, len(sched), same
+
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--scan", type=int, default=5)
+    ap.add_argument("--levels", type=int, default=3)
+    ap.add_argument("--map", type=int, default=2048)
+    args = ap.parse_args()
+    S = synth.make_streams(args.streams, args.scan + 1, seed=4321)
+    variants = {
+        "s68": (68, False, "id"), "s68_bidir": (68, True, "id"), "s67_bidir": (67, True, "id"),
+        "s68_split": (68, False, "split"), "s68_bidir_split": (68, True, "split"), "s67_bidir_split": (67, True, "split"),
+    }
+    tot = {k: [0, 0, 0, 0] for k in variants}
+    for s in range(args.streams):
+        pts = S.points[s, args.scan, : S.counts[s, args.scan]].astype(np.float64)
+        gt = S.gt[s, args.scan]
+        pose_cell = (args.map / 2 + gt[0] * 20.0, args.map / 2 + gt[1] * 20.0)
+        for lvl in range(args.levels):
+            x0, y0, x1, y1 = rays_for(pts, pose_cell, gt[2], lvl)
+            walks = [walk(x0, y0, int(a), int(b)) for a, b in zip(x1, y1)]
+            nb = len(walks)
+            xs = np.concatenate([[x0], x1]); ys = np.concatenate([[y0], y1])
+            tx0, tx1 = xs.min() // TILE, xs.max() // TILE
+            ty0, ty1 = ys.min() // TH, ys.max() // TH
+            for ty in range(ty0, ty1 + 1):
+                for tx in range(tx0, tx1 + 1):
+                    X0, Y0 = tx * TILE, ty * TH
+                    for g0 in range(0, nb, 64):
+                        lanes = []
+                        for l in range(64):
+                            b = g0 + l
+                            lanes.append(cells_in_tile(walks[b], X0, Y0) if b < nb else (np.zeros(0, int), np.zeros(0, int)))
+                        if not any(len(c[0]) for c in lanes):
+                            continue
+                        for k, (st, bw, od) in variants.items():
+                            r = wave_cycles(lanes, st, bw, od)
+                            for i in range(4):
+                                tot[k][i] += r[i]
+    base = tot["s68"][0]
+    for k, (cyc, ideal, ins, same) in tot.items():
+        print(f"{k:12s} cycles {cyc:9d} ({cyc / base:5.3f})  conflict-free {ideal:9d}  instructions {ins:8d}  same-address extra {same:8d}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1592,6 +1592,10 @@ constexpr int UPD_FIXED_WORDS = 2 * UPD_MARK_WORDS + 4;  // two mark buffers + 4
 
 // the free mark of one raster step: blind LDS atomicMin of the event code
 __device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) { atomicMin(p, ev); }
+// 32-bit LDS byte address of an LDS pointer, and back (the walk carries addresses in packed registers)
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+__device__ __forceinline__ unsigned lds_addr(unsigned *p) { return (unsigned)(size_t)(lds_u32 *)p; }
+__device__ __forceinline__ unsigned *lds_ptr(unsigned a) { return (unsigned *)(lds_u32 *)(size_t)a; }
 
 __device__ __forceinline__ int lane_rank(unsigned long long m)  // set lanes below this one
 {
@@ -1827,22 +1831,25 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 const int lb = w.x_major ? UPD_STRIDE : 1;
                 const int ia = w.a0 + (w.sa > 0 ? s0 : -s0) - A0, ib = w.b0 + (w.sb > 0 ? q : -q) - B0;
                 const int li = __mul24(ia, la) + __mul24(ib, lb);
-                // incremental walk on byte offsets into the mark array, f = da - 1 - error_b in [0, da)
-                // (backwards: g = error_b): the minor axis steps when f < db -- a subtract with borrow and
-                // two selects per step, four steps per trip
+                // incremental walk, f = da - 1 - error_b in [0, da) (backwards: g = error_b), packed with
+                // the LDS byte address of the step's mark word into ONE register, V = f << 18 | address
+                // (LDS addresses < 2^18, f < da < 2^13): the subtraction of db << 18 borrows exactly when
+                // f < db -- the minor axis steps -- and one select + add then moves both fields.  Three
+                // VALU per step plus the address mask, instead of five.
                 const int dab1 = w.sa * la * 4, dab21 = dab1 + w.sb * lb * 4;
                 const int dab = bwd ? -dab1 : dab1, dab2 = bwd ? -dab21 : dab21;
-                const int da_ = w.da, db_ = w.db;
-                int f = bwd ? err : da_ - 1 - err;
-                char *pm = reinterpret_cast<char *>(marks) + li * 4;
+                const int f0 = bwd ? err : w.da - 1 - err;
+                const unsigned vdn = (unsigned)w.db << 18;
+                const unsigned vk_major = (unsigned)dab;                            // f -= db, no minor step
+                const unsigned vk_minor = ((unsigned)w.da << 18) + (unsigned)dab2;  // f += da - db, minor step
+                unsigned v = ((unsigned)f0 << 18) + lds_addr(marks) + (unsigned)li * 4u;
                 int k = 0;
-#define S2D_WSTEP                                                                 \
-    do {                                                                          \
-        upd_mark(reinterpret_cast<unsigned *>(pm), ev); /* bresenhamCellFree */   \
-        unsigned fu_;                                                             \
-        const bool c_ = __builtin_sub_overflow((unsigned)f, (unsigned)db_, &fu_); \
-        f = (int)fu_ + (c_ ? da_ : 0);                                            \
-        pm += c_ ? dab2 : dab;                                                    \
+#define S2D_WSTEP                                                          \
+    do {                                                                   \
+        upd_mark(lds_ptr(v & 0x3FFFFu), ev); /* bresenhamCellFree */       \
+        unsigned vn_;                                                      \
+        const bool c_ = __builtin_sub_overflow(v, vdn, &vn_);              \
+        v = vn_ + (c_ ? vk_minor : vk_major);                              \
     } while (0)
                 for (; k + 3 < scnt; k += 4) {
                     S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
@@ -1851,7 +1858,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     S2D_WSTEP; S2D_WSTEP;
                 }
 #undef S2D_WSTEP
-                if (k < scnt) upd_mark(reinterpret_cast<unsigned *>(pm), ev);
+                if (k < scnt) upd_mark(lds_ptr(v & 0x3FFFFu), ev);
             }
             if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);
         }

@@ -60,8 +60,8 @@ PATCHES = {
     "plfastatan": [("plicp_kernels.hip", '#include "detmath.h"\n',
                     '#include "detmath.h"\n#define sdm_atan2(y, x) ((double)atan2f((float)(y), (float)(x)))\n'
                     '#define sdm_atan(x) ((double)atanf((float)(x)))\n')],
-    "nowalk": [(K, "                if (lo_i > hi_i) continue;\n                any = true;\n",
-                "                if (lo_i > hi_i) continue;\n                any = true;\n                continue;\n")],
+    "nowalk": [(K, "                if (lo_i > hi_i) continue;\n                anyv = 1u;\n",
+                "                if (lo_i > hi_i) continue;\n                anyv = 1u;\n                continue;\n")],
     "nosetup": [(K, "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n",
                  "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n                continue;\n")],
     "noraster": [(K, "                const int4 gb = gbox[b0 >> 6];\n", "                if (b0 >= 0) break;\n                const int4 gb = gbox[b0 >> 6];\n")],

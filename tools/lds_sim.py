@@ -67,7 +67,7 @@ def wave_cycles(fan_cells, stride, bwd_odd, order="id"):
     for l in range(64):
         lx, ly = lanes_cells[l]
         a = ly * stride + lx
-        if bwd_odd and (l & 1):
+        if (bwd_odd == 1 and (l & 1)) or (bwd_odd == 2 and l >= 32) or (bwd_odd == 3 and (l & 2)):
             a = a[::-1]
         addrs.append(a)
     # instruction schedule: 4-step trips, then one 2-step trip, then the last single step
@@ -106,11 +106,15 @@ def main():
     ap.add_argument("--scan", type=int, default=5)
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--map", type=int, default=2048)
+    ap.add_argument("--detail", default="", help="variant: break its cycles down by level and origin tile")
     args = ap.parse_args()
+    det = {}
+    util = dict(c_tests=0, c_chunks=0, c_cycles=0, c_instr=0, pairs=0, bbox_lanes=0, walk_lanes=0, lane_steps=0, walk_instr=0, waves_with_walk=0)
     S = synth.make_streams(args.streams, args.scan + 1, seed=4321)
     variants = {
-        "s68": (68, False, "id"), "s68_bidir": (68, True, "id"), "s67_bidir": (67, True, "id"),
-        "s68_split": (68, False, "split"), "s68_bidir_split": (68, True, "split"), "s67_bidir_split": (67, True, "split"),
+        "s68": (68, 0, "id"), "s68_bidir_split": (68, 1, "split"), "s67_bidir_split": (67, 1, "split"),
+        "s68_grpdir_id": (68, 2, "id"), "s67_grpdir_id": (67, 2, "id"), "s67_grpdir_split": (67, 2, "split"),
+        "s68_pairdir_split": (68, 3, "split"), "s67_pairdir_split": (67, 3, "split"),
     }
     tot = {k: [0, 0, 0, 0] for k in variants}
     for s in range(args.streams):
@@ -127,20 +131,60 @@ def main():
             for ty in range(ty0, ty1 + 1):
                 for tx in range(tx0, tx1 + 1):
                     X0, Y0 = tx * TILE, ty * TH
+                    for wv in range(4):
+                        items = []
+                        for g0 in range(64 * wv, nb, 256):
+                            fb = [(min(x0, x1[b]), min(y0, y1[b]), max(x0, x1[b]), max(y0, y1[b])) for b in range(g0, min(g0 + 64, nb))]
+                            if max(f[2] for f in fb) < X0 or min(f[0] for f in fb) >= X0 + TILE or max(f[3] for f in fb) < Y0 or min(f[1] for f in fb) >= Y0 + TH:
+                                continue
+                            util["c_tests"] += 1
+                            for b in range(g0, min(g0 + 64, nb)):
+                                c = cells_in_tile(walks[b], X0, Y0)
+                                if len(c[0]):
+                                    items.append(c)
+                        for c0 in range(0, len(items), 64):
+                            ch = items[c0:c0 + 64]
+                            ch = ch + [(np.zeros(0, int), np.zeros(0, int))] * (64 - len(ch))
+                            util["c_chunks"] += 1
+                            r = wave_cycles(ch, 68, 1, "id")
+                            util["c_cycles"] += r[0]; util["c_instr"] += r[2]
                     for g0 in range(0, nb, 64):
+                        fb = [(x0, y0, x0, y0)] + [(min(x0, x1[b]), min(y0, y1[b]), max(x0, x1[b]), max(y0, y1[b]))
+                                                   for b in range(g0, min(g0 + 64, nb))]
+                        gx0 = min(f[0] for f in fb); gy0 = min(f[1] for f in fb)
+                        gx1 = max(f[2] for f in fb); gy1 = max(f[3] for f in fb)
+                        if gx1 < X0 or gx0 >= X0 + TILE or gy1 < Y0 or gy0 >= Y0 + TH:
+                            continue
+                        util["pairs"] += 1
+                        util["bbox_lanes"] += sum(1 for f in fb[1:] if not (f[2] < X0 or f[0] >= X0 + TILE or f[3] < Y0 or f[1] >= Y0 + TH))
                         lanes = []
                         for l in range(64):
                             b = g0 + l
                             lanes.append(cells_in_tile(walks[b], X0, Y0) if b < nb else (np.zeros(0, int), np.zeros(0, int)))
-                        if not any(len(c[0]) for c in lanes):
+                        nw = [len(c[0]) for c in lanes]
+                        util["walk_lanes"] += sum(1 for k in nw if k)
+                        util["lane_steps"] += sum(nw)
+                        if not any(nw):
                             continue
+                        util["waves_with_walk"] += 1
                         for k, (st, bw, od) in variants.items():
                             r = wave_cycles(lanes, st, bw, od)
                             for i in range(4):
                                 tot[k][i] += r[i]
+                            if k == args.detail:
+                                key = (lvl, X0 <= x0 < X0 + TILE and Y0 <= y0 < Y0 + TH)
+                                d = det.setdefault(key, [0, 0, 0, 0])
+                                for i in range(4):
+                                    d[i] += r[i]
+    print(util, "setup lanes busy %.3f (bbox) %.3f (walk) of 64 per pair" % (util["bbox_lanes"] / util["pairs"] / 64, util["walk_lanes"] / util["pairs"] / 64))
     base = tot["s68"][0]
     for k, (cyc, ideal, ins, same) in tot.items():
+        if k == "s68":
+            print(f"walk lane utilisation {util['lane_steps'] / (64 * ins):.3f} ({util['lane_steps']} lane-steps, {ins} walk instructions)")
         print(f"{k:12s} cycles {cyc:9d} ({cyc / base:5.3f})  conflict-free {ideal:9d}  instructions {ins:8d}  same-address extra {same:8d}")
+    for (lvl, org), (cyc, ideal, ins, same) in sorted(det.items()):
+        print(f"  {args.detail} level {lvl} {'origin tile' if org else 'other tiles'}: cycles {cyc:8d} conflict-free {ideal:8d} "
+              f"instructions {ins:7d} same-address extra {same:7d}")
 
 
 if __name__ == "__main__":

@@ -6,6 +6,7 @@ export TMPDIR=/tmp
 cd /tmp
 for v in "$@"; do
   if [ "$v" = main ]; then lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/libslam2d.so; else lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/libslam2d_$v.so; fi
+  [ -f "$lib" ] || { echo "missing $lib"; exit 1; }
   OUT=$ROOT/gpurun_out/pmcab_${TAG}_$v; mkdir -p "$OUT"
   i=0
   for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \

@@ -1548,7 +1548,7 @@ constexpr int UPD_STRIDE = S2D_UPD_STRIDE;
 #define S2D_UPD_TH 32
 #endif
 #ifndef S2D_UPD_MINB
-#define S2D_UPD_MINB 1  // __launch_bounds__ min workgroups per CU (caps VGPRs)
+#define S2D_UPD_MINB 8  // __launch_bounds__ min workgroups per CU: 8 x 4 waves caps the VGPRs at 64 (full occupancy)
 #endif
 constexpr int UPD_TH = S2D_UPD_TH;                    // LDS tile height (a multiple of the storage TILE_H)
 static_assert(UPD_TH % TILE_H == 0, "an LDS tile covers whole storage tiles");
@@ -1565,6 +1565,12 @@ constexpr int UPD_QUADS = TILE * UPD_TH / 4 / UPD_THREADS;  // apply quads per t
 // depend on within one scan.  A quad's marks are carried in registers as 12 bits: bit c "marked",
 // bit 4 + c "odd event word", bit 8 + c "hit" for its cells c = 0..3.
 // GridMapLogOddsFunctions (GridMapLogOdds.h:108-129) applied to one marked cell:
+// bit k of m set ? a : b, as a bitwise select on the float bits (no compare, no exec-mask branch)
+__device__ __forceinline__ float bit_select(unsigned m, int k, float a, float b)
+{
+    const int sel = ((int)(m << (31 - k))) >> 31;  // 0 or -1
+    return __int_as_float((__float_as_int(a) & sel) | (__float_as_int(b) & ~sel));
+}
 __device__ __forceinline__ float apply_cell(float l, unsigned odd, unsigned hit, float lf, float lo)
 {
     if (!hit) return l + lf;   // updateSetFree (:120-124)
@@ -1758,92 +1764,110 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     unsigned touched = 0;
 
     const int ntx = tx1 - tx0 + 1, ntiles = ntx * (ty1 - ty0 + 1);
+    const int nfans = ((n + UPD_THREADS - 1) / UPD_THREADS) * (UPD_THREADS / 64);  // groups with a box in gbox
     const int my_tiles = ntiles > part ? (ntiles - part + parts - 1) / parts : 0;
     // Two-stage pipeline over this workgroup's tiles t_i = part + i * parts, ONE barrier per tile:
-    //   iteration i: raster tile i into buffer i & 1 -> apply tile i - 1 from registers (its cell loads
-    //   were issued one raster earlier) -> barrier -> read tile i's marks into registers, issue the
+    //   iteration i: raster tile i into buffer i & 1 -> apply tile i - 1 from registers (its cell
+    //   loads were issued one raster earlier) -> barrier -> read tile i's marks into registers, issue the
     //   loads of its marked quads and restore the words just read to "no mark".
     // Every mark word is read and restored by the thread that owns its quad (a hit-bit word by one
     // lane of the 8 that read it, all in one wave, after the read), so a buffer is clean again before
-    // the barrier of iteration i + 1 that precedes its next raster; a tile without marks wrote
-    // nothing.  s_any[buf] holds the number (i + 1) of the last tile of that buffer that had a mark,
-    // so it needs no reset.  The barrier only waits for LDS traffic (lds_barrier), so the loads and the
-    // previous tile's stores stay in flight across it.
+    // the barrier of iteration i + 1 that precedes its next raster; a tile without marks wrote nothing.
+    // s_any[buf] holds the number (i + 1) of the last tile of that buffer that had a mark, so it needs no
+    // reset.  The barrier only waits for LDS traffic (lds_barrier), so the loads and the previous tile's
+    // stores stay in flight across it.  (Skipping the tiles no fan group reaches outright -- no barrier,
+    // buffers alternating over the rastered tiles only -- measured no faster: the skeleton of an empty
+    // tile is now a ballot, and the extra state cost the kernel two spilled VGPRs.)
     float4 ql[UPD_QUADS];      // pending tile: log-odds of the marked quads (loads in flight)
     unsigned qb[UPD_QUADS];    // pending tile: 12 mark bits per quad (see apply_cell)
     float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)
     for (int i = 0; i <= my_tiles; ++i) {
-        const int buf = i & 1;
-        unsigned *marks = smem + buf * UPD_MARK_WORDS;
-        unsigned *hitb = marks + UPD_TILE_WORDS;
         const int t = part + i * parts;
         const int ty = ty0 + t / ntx, tx = tx0 + t % ntx;
         const int X0 = tx * TILE, Y0 = ty * UPD_TH;
         const int X1 = X0 + TILE, Y1 = Y0 + UPD_TH;
+        const int buf = i & 1;
+        unsigned *marks = smem + buf * UPD_MARK_WORDS;
+        unsigned *hitb = marks + UPD_TILE_WORDS;
         if (i < my_tiles) {
             unsigned anyv = 0u;  // a VGPR flag: no exec-mask merging of a divergent bool
-            for (int b0 = wave_beam0; (b0 & ~255) < n; b0 += UPD_THREADS) {
-                // wave-uniform fan-group test (scalar)
-                const int4 gb = gbox[b0 >> 6];
-                const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
-                const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
-                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
-                const int b = fan_beam(b0, lane);
-                unsigned r;
-                if constexpr (RREG > 0) {
-                    const int k = b0 >> 8;
-                    r = k == 0 ? rr0 : (k == 1 ? rr1 : (k == 2 ? rr2 : (k == 3 ? rr3 : rr4)));
-                }
-                else r = b < n ? rays[b] : RAY_INVALID;
-                if (r == RAY_INVALID) continue;
-                const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-                if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
-                if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {  // bresenhamCellOcc (:266)
-                    const int c = (y1 - Y0) * TILE + (x1 - X0);
-                    atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
-                    atomicOr(&hitb[c >> 5], 1u << (c & 31));
+            // the fan groups whose box meets the tile, one bit each: lane f tests group f, one ballot (the
+            // scalar box test of every group of the wave on every tile cost ~20 SALU a time, most of them
+            // on tiles no fan reaches); groups past the first 64 (scans of > 4096 points) test their box alone
+            unsigned long long fm;
+            {
+                int ol = lane;  // opaque: the lane's box address is not hoisted into a VGPR held across tiles
+                asm volatile("" : "+v"(ol));
+                const int4 gb = gbox[min(ol, nfans - 1)];
+                fm = __ballot((ol < nfans) & (gb.z >= X0) & (gb.x < X1) & (gb.w >= Y0) & (gb.y < Y1));
+            }
+            {
+                for (int b0 = wave_beam0; (b0 & ~255) < n; b0 += UPD_THREADS) {
+                    const int fi = b0 >> 6;  // wave-uniform
+                    if (fi < 64) {
+                        if (!((fm >> fi) & 1ull)) continue;
+                    } else {
+                        const int4 gb = gbox[fi];
+                        const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
+                        const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
+                        if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
+                    }
+                    const int b = fan_beam(b0, lane);
+                    unsigned r;
+                    if constexpr (RREG > 0) {
+                        const int k = b0 >> 8;
+                        r = k == 0 ? rr0 : (k == 1 ? rr1 : (k == 2 ? rr2 : (k == 3 ? rr3 : rr4)));
+                    }
+                    else r = b < n ? rays[b] : RAY_INVALID;
+                    if (r == RAY_INVALID) continue;
+                    const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+                    if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
+                    if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {  // bresenhamCellOcc (:266)
+                        const int c = (y1 - Y0) * TILE + (x1 - X0);
+                        atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
+                        atomicOr(&hitb[c >> 5], 1u << (c & 31));
+                        anyv = 1u;
+                    }
+                    const RayWalk w = ray_walk(x0, y0, x1, y1);
+                    // the tile in (major, minor) order, selected before ONE clip (lanes of a fan that straddles
+                    // a diagonal differ in x_major)
+                    const int A0 = w.x_major ? X0 : Y0, A1 = w.x_major ? X1 : Y1;
+                    const int B0 = w.x_major ? Y0 : X0, B1 = w.x_major ? Y1 : X1;
+                    int lo_i, hi_i;
+                    if (!walk_range(w, A0, A1, B0, B1, lo_i, hi_i)) continue;
+                    if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
+                    if (lo_i > hi_i) continue;
                     anyv = 1u;
-                }
-                const RayWalk w = ray_walk(x0, y0, x1, y1);
-                // the tile in (major, minor) order, selected before ONE clip (lanes of a fan that straddles
-                // a diagonal differ in x_major)
-                const int A0 = w.x_major ? X0 : Y0, A1 = w.x_major ? X1 : Y1;
-                const int B0 = w.x_major ? Y0 : X0, B1 = w.x_major ? Y1 : X1;
-                int lo_i, hi_i;
-                if (!walk_range(w, A0, A1, B0, B1, lo_i, hi_i)) continue;
-                if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
-                if (lo_i > hi_i) continue;
-                anyv = 1u;
-                const int scnt = hi_i - lo_i + 1;     // free steps of this beam inside the tile
-                // Odd lanes walk their segment backwards, from hi_i down to lo_i (the same cells; the step
-                // below is its own inverse in g = da - 1 - f): at one instruction neighbouring beams then sit
-                // at different radii, so near the scan origin half as many lanes hit one LDS word (the
-                // atomics to one address serialise).
-                const bool bwd = (lane & 1) != 0;
-                const int s0 = bwd ? hi_i : lo_i;
-                // (s0, db, q, da < 2^15 and the tile offsets < 2^7: 24-bit multiplies throughout)
-                const unsigned num = (unsigned)w.e0 + __umul24((unsigned)s0, (unsigned)w.db);
-                const int q = (int)udiv_small(num, (unsigned)w.da);
-                const int err = (int)(num - __umul24((unsigned)q, (unsigned)w.da));
-                const unsigned ev = 2u * (unsigned)b + 1u;
-                // LDS index of step s0 and its increments along the major / minor axis
-                const int la = w.x_major ? 1 : UPD_STRIDE;
-                const int lb = w.x_major ? UPD_STRIDE : 1;
-                const int ia = w.a0 + (w.sa > 0 ? s0 : -s0) - A0, ib = w.b0 + (w.sb > 0 ? q : -q) - B0;
-                const int li = __mul24(ia, la) + __mul24(ib, lb);
-                // incremental walk, f = da - 1 - error_b in [0, da) (backwards: g = error_b), packed with
-                // the LDS byte address of the step's mark word into ONE register, V = f << 18 | address
-                // (LDS addresses < 2^18, f < da < 2^13): the subtraction of db << 18 borrows exactly when
-                // f < db -- the minor axis steps -- and one select + add then moves both fields.  Three
-                // VALU per step plus the address mask, instead of five.
-                const int dab1 = w.sa * la * 4, dab21 = dab1 + w.sb * lb * 4;
-                const int dab = bwd ? -dab1 : dab1, dab2 = bwd ? -dab21 : dab21;
-                const int f0 = bwd ? err : w.da - 1 - err;
-                const unsigned vdn = (unsigned)w.db << 18;
-                const unsigned vk_major = (unsigned)dab;                            // f -= db, no minor step
-                const unsigned vk_minor = ((unsigned)w.da << 18) + (unsigned)dab2;  // f += da - db, minor step
-                unsigned v = ((unsigned)f0 << 18) + lds_addr(marks) + (unsigned)li * 4u;
-                int k = 0;
+                    const int scnt = hi_i - lo_i + 1;     // free steps of this beam inside the tile
+                    // Odd lanes walk their segment backwards, from hi_i down to lo_i (the same cells; the step
+                    // below is its own inverse in g = da - 1 - f): at one instruction neighbouring beams then sit
+                    // at different radii, so near the scan origin half as many lanes hit one LDS word (the
+                    // atomics to one address serialise).
+                    const bool bwd = (lane & 1) != 0;
+                    const int s0 = bwd ? hi_i : lo_i;
+                    // (s0, db, q, da < 2^15 and the tile offsets < 2^7: 24-bit multiplies throughout)
+                    const unsigned num = (unsigned)w.e0 + __umul24((unsigned)s0, (unsigned)w.db);
+                    const int q = (int)udiv_small(num, (unsigned)w.da);
+                    const int err = (int)(num - __umul24((unsigned)q, (unsigned)w.da));
+                    const unsigned ev = 2u * (unsigned)b + 1u;
+                    // LDS index of step s0 and its increments along the major / minor axis
+                    const int la = w.x_major ? 1 : UPD_STRIDE;
+                    const int lb = w.x_major ? UPD_STRIDE : 1;
+                    const int ia = w.a0 + (w.sa > 0 ? s0 : -s0) - A0, ib = w.b0 + (w.sb > 0 ? q : -q) - B0;
+                    const int li = __mul24(ia, la) + __mul24(ib, lb);
+                    // incremental walk, f = da - 1 - error_b in [0, da) (backwards: g = error_b), packed with
+                    // the LDS byte address of the step's mark word into ONE register, V = f << 18 | address
+                    // (LDS addresses < 2^18, f < da < 2^13): the subtraction of db << 18 borrows exactly when
+                    // f < db -- the minor axis steps -- and one select + add then moves both fields.  Three
+                    // VALU per step plus the address mask, instead of five.
+                    const int dab1 = w.sa * la * 4, dab21 = dab1 + w.sb * lb * 4;
+                    const int dab = bwd ? -dab1 : dab1, dab2 = bwd ? -dab21 : dab21;
+                    const int fw0 = bwd ? err : w.da - 1 - err;
+                    const unsigned vdn = (unsigned)w.db << 18;
+                    const unsigned vk_major = (unsigned)dab;                            // f -= db, no minor step
+                    const unsigned vk_minor = ((unsigned)w.da << 18) + (unsigned)dab2;  // f += da - db, minor step
+                    unsigned v = ((unsigned)fw0 << 18) + lds_addr(marks) + (unsigned)li * 4u;
+                    int k = 0;
 #define S2D_WSTEP                                                          \
     do {                                                                   \
         upd_mark(lds_ptr(v & 0x3FFFFu), ev); /* bresenhamCellFree */       \
@@ -1851,14 +1875,15 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         const bool c_ = __builtin_sub_overflow(v, vdn, &vn_);              \
         v = vn_ + (c_ ? vk_minor : vk_major);                              \
     } while (0)
-                for (; k + 3 < scnt; k += 4) {
-                    S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
-                }
-                for (; k + 1 < scnt; k += 2) {
-                    S2D_WSTEP; S2D_WSTEP;
-                }
+                    for (; k + 3 < scnt; k += 4) {
+                        S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
+                    }
+                    for (; k + 1 < scnt; k += 2) {
+                        S2D_WSTEP; S2D_WSTEP;
+                    }
 #undef S2D_WSTEP
-                if (k < scnt) upd_mark(lds_ptr(v & 0x3FFFFu), ev);
+                    if (k < scnt) upd_mark(lds_ptr(v & 0x3FFFFu), ev);
+                }
             }
             if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);
         }
@@ -1880,11 +1905,18 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
                 int uv[4];
+                // apply_cell on the 4 cells without branches: every candidate value computed, then picked by
+                // bit selects on the sign-extended mark bits (v_bfe_i32 + v_bfi_b32: two VALU per choice; the
+                // branchy form compiled to exec-mask code around each cell)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    nv[c] = ((mb >> c) & 1u) ? apply_cell(lv[c], (mb >> (4 + c)) & 1u, (mb >> (8 + c)) & 1u, lf, lo)
-                                             : lv[c];
-                    uv[c] = ((mb >> (8 + c)) & 1u) ? mark_occ : mark_free;
+                    const float l = lv[c];
+                    const float t = l + lf;                       // updateSetFree
+                    const float u = t - lf;                       // ... then updateUnsetFree
+                    const float h = bit_select(mb, 4 + c, u, l);  // an earlier beam freed the hit cell
+                    const float oc = h < 50.0f ? h + lo : h;      // updateSetOccupied
+                    nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);
+                    uv[c] = __float_as_int(bit_select(mb, 8 + c, __int_as_float(mark_occ), __int_as_float(mark_free)));
                 }
                 // log-odds: the whole quad was loaded, so it is stored whole (one instruction; unmarked
                 // cells rewrite their own value); updateIndex: whole when every cell is marked, else

@@ -17,8 +17,13 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   nosetup    WRONG RESULTS  hs_update_kernel keeps the fan-group culling of every tile, skips every ray
   noraster   WRONG RESULTS  hs_update_kernel skips the raster loop (tile loop skeleton: clear, barriers)
   ktnorender WRONG RESULTS  kt_addscans_kernel clears, loads and stores its tiles but renders no item
-  lds6       same results   hs_update_kernel with 2.5 KB of unused LDS (7 -> 6 workgroups per CU: occupancy price)
-  lds5       same results   hs_update_kernel with 10 KB of unused LDS (5 workgroups per CU)
+  lds6       same results   hs_update_kernel with 8.2 KB of unused LDS (8 -> 6 workgroups per CU: occupancy price)
+  lds4       same results   hs_update_kernel with 21 KB of unused LDS (4 workgroups per CU)
+  frozen     WRONG RESULTS  hs_match_kernel runs no Gauss-Newton iteration (pose = hint): the rays no longer depend
+                            on the map, so an update-kernel pricing variant built as frozen__<variant> and timed
+                            against frozen alone is not confounded by a drifting match
+  noapplymath WRONG RESULTS hs_update_kernel's apply stores l + lf for every marked cell (prices the cell math)
+  fullstore  WRONG RESULTS  hs_update_kernel stores whole updateIndex quads (prices the per-cell partial stores)
   ktnoswar   WRONG RESULTS  kt_addscans_kernel dword render writes the kernel bytes without the byte max
   ktnomerge  WRONG RESULTS  kt_build_kernel skips the 64-bit CAS merge of its tile into the match grid
   ktstore    WRONG RESULTS  kt_build_kernel merges with plain stores instead of compare-and-swap
@@ -66,10 +71,10 @@ PATCHES = {
                  "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n                continue;\n")],
     "noraster": [(K, "                const int4 gb = gbox[b0 >> 6];\n", "                if (b0 >= 0) break;\n                const int4 gb = gbox[b0 >> 6];\n")],
     "ktnorender": [("karto_kernels.hip", "kt_render_items_dw(tileb, sitem, c0, c1,", "kt_render_items_dw(tileb, sitem, c0, c0,")],
-    "lds6": [("hector_capi.hip", "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));\n    const bool single",
-              "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points)) + 2560;\n    const bool single")],
-    "lds5": [("hector_capi.hip", "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));\n    const bool single",
-              "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points)) + 10240;\n    const bool single")],
+    "lds6": [("hector_capi.hip", "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));\n}",
+              "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points) + 2100);\n}")],
+    "lds4": [("hector_capi.hip", "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));\n}",
+              "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points) + 5430);\n}")],
     "ktnomerge": [("karto_kernels.hip", "    for (int t0 = lane; t0 < nw; t0 += 64 * 8) {\n        unsigned long long want[8], old[8];",
                    "    if (nw > 0) return true;\n    for (int t0 = lane; t0 < nw; t0 += 64 * 8) {\n        unsigned long long want[8], old[8];")],
     "ktstore": [("karto_kernels.hip", "                old[u] = atomicCAS(gw + wbase + r * wsw + q, 0ull, want[u]);",
@@ -98,19 +103,27 @@ PATCHES = {
                  "    const float4 *row = reinterpret_cast<const float4 *>(T + lane * SEQ_STRIDE);\n    const int c4 = cnt >> 2;\n    float r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;"),
                 (K, "    for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];\n    return run;",
                  "    for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];\n    return run + (r1 + (r2 + r3));")],
+    "frozen": [(K, "            for (int it = 0; it <= iters; ++it) {\n                if (in_regs) {",
+                "            for (int it = 0; it <= iters && false; ++it) {\n                if (in_regs) {")],
+    "noapplymath": [(K, "                    nv[c] = ((mb >> c) & 1u) ? apply_cell(lv[c], (mb >> (4 + c)) & 1u, (mb >> (8 + c)) & 1u, lf, lo)\n                                             : lv[c];",
+                     "                    nv[c] = lv[c] + lf;")],
+    "fullstore": [(K, "                if ((mb & 15u) == 15u) {\n                    *reinterpret_cast<int4 *>(&tu[o])",
+                   "                if (true) {\n                    *reinterpret_cast<int4 *>(&tu[o])")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 
 
 def build(variant: str) -> str:
-    if variant not in PATCHES:
-        raise SystemExit(f"unknown variant {variant!r}; known: {', '.join(sorted(PATCHES))}")
+    parts = variant.split("__")  # a__b: both patch lists (e.g. frozen__noapply)
+    for v in parts:
+        if v not in PATCHES:
+            raise SystemExit(f"unknown variant {v!r}; known: {', '.join(sorted(PATCHES))}")
     tmp = tempfile.mkdtemp()
     try:
         src = os.path.join(tmp, "creating-2d-laser-slam-from-scratch_amd", "csrc")
         shutil.copytree(os.path.join(PKG, "csrc"), src)
         shutil.copytree(os.path.join(REPO, "include"), os.path.join(tmp, "include"))
-        for fname, old, new in PATCHES[variant]:
+        for fname, old, new in [p for v in parts for p in PATCHES[v]]:
             p = os.path.join(src, fname)
             text = open(p).read()
             if text.count(old) != 1:

@@ -1799,7 +1799,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 int ol = lane;  // opaque: the lane's box address is not hoisted into a VGPR held across tiles
                 asm volatile("" : "+v"(ol));
                 const int4 gb = gbox[min(ol, nfans - 1)];
-                fm = __ballot((ol < nfans) & (gb.z >= X0) & (gb.x < X1) & (gb.w >= Y0) & (gb.y < Y1));
+                fm = __ballot((int)(ol < nfans) & (int)(gb.z >= X0) & (int)(gb.x < X1) & (int)(gb.w >= Y0) &
+                              (int)(gb.y < Y1));
             }
             {
                 for (int b0 = wave_beam0; (b0 & ~255) < n; b0 += UPD_THREADS) {
@@ -1819,9 +1820,12 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                         r = k == 0 ? rr0 : (k == 1 ? rr1 : (k == 2 ? rr2 : (k == 3 ? rr3 : rr4)));
                     }
                     else r = b < n ? rays[b] : RAY_INVALID;
-                    if (r == RAY_INVALID) continue;
+                    // the tests below are combined with bitwise ors: one divergent branch (exec-mask save,
+                    // test, restore: SALU work) per early exit instead of one per condition
                     const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
-                    if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
+                    if ((int)(r == RAY_INVALID) | (int)(max(x0, x1) < X0) | (int)(min(x0, x1) >= X1) |
+                        (int)(max(y0, y1) < Y0) | (int)(min(y0, y1) >= Y1))
+                        continue;
                     if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {  // bresenhamCellOcc (:266)
                         const int c = (y1 - Y0) * TILE + (x1 - X0);
                         atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
@@ -1834,9 +1838,9 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     const int A0 = w.x_major ? X0 : Y0, A1 = w.x_major ? X1 : Y1;
                     const int B0 = w.x_major ? Y0 : X0, B1 = w.x_major ? Y1 : X1;
                     int lo_i, hi_i;
-                    if (!walk_range(w, A0, A1, B0, B1, lo_i, hi_i)) continue;
+                    const bool met = walk_range(w, A0, A1, B0, B1, lo_i, hi_i);
                     if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)
-                    if (lo_i > hi_i) continue;
+                    if ((int)!met | (int)(lo_i > hi_i)) continue;
                     anyv = 1u;
                     const int scnt = hi_i - lo_i + 1;     // free steps of this beam inside the tile
                     // Odd lanes walk their segment backwards, from hi_i down to lo_i (the same cells; the step
@@ -1875,11 +1879,18 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         const bool c_ = __builtin_sub_overflow(v, vdn, &vn_);              \
         v = vn_ + (c_ ? vk_minor : vk_major);                              \
     } while (0)
-                    for (; k + 3 < scnt; k += 4) {
-                        S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
+                    // eight steps per trip (the loop control -- a scalar counter, the exec mask update and
+                    // the branch -- is per trip), then at most one trip of four and of two
+                    for (; k + 7 < scnt; k += 8) {
+                        S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
                     }
-                    for (; k + 1 < scnt; k += 2) {
+                    if (k + 3 < scnt) {
+                        S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
+                        k += 4;
+                    }
+                    if (k + 1 < scnt) {
                         S2D_WSTEP; S2D_WSTEP;
+                        k += 2;
                     }
 #undef S2D_WSTEP
                     if (k < scnt) upd_mark(lds_ptr(v & 0x3FFFFu), ev);

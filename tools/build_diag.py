@@ -14,8 +14,8 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   gmnowalk   WRONG RESULTS  gm_compute_kernel clips every line to the tile but skips the walk
   nowalk     WRONG RESULTS  hs_update_kernel clips every ray to the tile but skips the Bresenham walk
   plfastatan WRONG RESULTS  pl_icp_kernel uses float atan / atan2 (prices the exact double ones)
-  nosetup    WRONG RESULTS  hs_update_kernel keeps the fan-group culling of every tile, skips every ray
-  noraster   WRONG RESULTS  hs_update_kernel skips the raster loop (tile loop skeleton: clear, barriers)
+  nosetup    WRONG RESULTS  hs_update_kernel keeps the fan-group culling of every tile, skips every ray (the
+                            tile loop skeleton: culling ballot, barriers, empty applies)
   ktnorender WRONG RESULTS  kt_addscans_kernel clears, loads and stores its tiles but renders no item
   lds6       same results   hs_update_kernel with 8.2 KB of unused LDS (8 -> 6 workgroups per CU: occupancy price)
   lds4       same results   hs_update_kernel with 21 KB of unused LDS (4 workgroups per CU)
@@ -65,11 +65,10 @@ PATCHES = {
     "plfastatan": [("plicp_kernels.hip", '#include "detmath.h"\n',
                     '#include "detmath.h"\n#define sdm_atan2(y, x) ((double)atan2f((float)(y), (float)(x)))\n'
                     '#define sdm_atan(x) ((double)atanf((float)(x)))\n')],
-    "nowalk": [(K, "                if (lo_i > hi_i) continue;\n                anyv = 1u;\n",
-                "                if (lo_i > hi_i) continue;\n                anyv = 1u;\n                continue;\n")],
-    "nosetup": [(K, "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n",
-                 "                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;\n                continue;\n")],
-    "noraster": [(K, "                const int4 gb = gbox[b0 >> 6];\n", "                if (b0 >= 0) break;\n                const int4 gb = gbox[b0 >> 6];\n")],
+    "nowalk": [(K, "                    if ((int)!met | (int)(lo_i > hi_i)) continue;\n                    anyv = 1u;\n",
+                "                    if ((int)!met | (int)(lo_i > hi_i)) continue;\n                    anyv = 1u;\n                    continue;\n")],
+    "nosetup": [(K, "                        if (!((fm >> fi) & 1ull)) continue;\n",
+                 "                        if (!((fm >> fi) & 1ull)) continue;\n                        continue;\n")],
     "ktnorender": [("karto_kernels.hip", "kt_render_items_dw(tileb, sitem, c0, c1,", "kt_render_items_dw(tileb, sitem, c0, c0,")],
     "lds6": [("hector_capi.hip", "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));\n}",
               "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points) + 2100);\n}")],
@@ -92,8 +91,8 @@ PATCHES = {
     "phase2": [(K, "    load_exptab();\n    __syncthreads();\n    const float *scells",
                 "    if ((blockIdx.x >> 8) & 1) { __builtin_amdgcn_s_sleep(127); __builtin_amdgcn_s_sleep(127); }\n"
                 "    load_exptab();\n    __syncthreads();\n    const float *scells")],
-    "noorigin": [(K, "                if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)\n                if (lo_i > hi_i) continue;",
-                  "                if (hi_i > w.da - 1) hi_i = w.da - 1;  // steps 0..da-1 are freed (:277-298)\n                if (lo_i < 8) lo_i = 8;\n                if (lo_i > hi_i) continue;")],
+    "noorigin": [(K, "                    if ((int)!met | (int)(lo_i > hi_i)) continue;\n",
+                  "                    if (lo_i < 8) lo_i = 8;\n                    if (!met | (lo_i > hi_i)) continue;\n")],
     "nohitbit": [(K, "                    atomicOr(&hitb[c >> 5], 1u << (c & 31));\n", "                    (void)c;\n")],
     "seqnochain": [(K, "    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);",
                     "    if ((tid >> 6) == cw && lane < 9) run = run + T[lane * SEQ_STRIDE];")],

@@ -53,10 +53,12 @@ constexpr int CELL_BLK = 4;
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
-inline int tile_cell(int lx, int ly)  // (lx, ly) inside the tile -> its word inside a plane
+inline int tile_cell(int lx, int ly)  // (lx, ly) inside the tile (>= 0) -> its word inside a plane
 {
-    return ((ly / CELL_BLK) * (TILE / CELL_BLK) + (lx / CELL_BLK)) * (CELL_BLK * CELL_BLK) + (ly % CELL_BLK) * CELL_BLK +
-           (lx % CELL_BLK);
+    // unsigned: shifts and masks, whatever the compiler knows of the signs
+    const unsigned x = (unsigned)lx, y = (unsigned)ly;
+    return (int)(((y / CELL_BLK) * (TILE / CELL_BLK) + (x / CELL_BLK)) * (CELL_BLK * CELL_BLK) + (y % CELL_BLK) * CELL_BLK +
+                 (x % CELL_BLK));
 }
 
 // word index of cell (x, y)'s log-odds inside its level; its updateIndex is TILE_CELLS words later

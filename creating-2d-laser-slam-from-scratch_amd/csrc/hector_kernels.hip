@@ -973,7 +973,7 @@ __device__ __forceinline__ unsigned udiv_rcp(unsigned n, unsigned d, float rcp_d
     if (r >= (int)d) ++q;
     return q;
 }
-__device__ __forceinline__ unsigned udiv_small(unsigned n, unsigned d)
+__device__ __forceinline__ unsigned udiv_small(unsigned n, unsigned d, unsigned &rem)  // quotient and remainder
 {
 #if S2D_FAST_UDIV
     unsigned q = (unsigned)((float)n * __builtin_amdgcn_rcpf((float)d));
@@ -982,9 +982,14 @@ __device__ __forceinline__ unsigned udiv_small(unsigned n, unsigned d)
         --q;
         r += (int)d;
     }
-    if (r >= (int)d) ++q;
+    if (r >= (int)d) {
+        ++q;
+        r -= (int)d;
+    }
+    rem = (unsigned)r;  // (the caller's own n - q * d compiled to a quarter-rate 32-bit multiply)
     return q;
 #else
+    rem = n % d;
     return n / d;
 #endif
 }
@@ -1553,6 +1558,10 @@ constexpr int UPD_STRIDE = S2D_UPD_STRIDE;
 constexpr int UPD_TH = S2D_UPD_TH;                    // LDS tile height (a multiple of the storage TILE_H)
 static_assert(UPD_TH % TILE_H == 0, "an LDS tile covers whole storage tiles");
 constexpr int UPD_TILE_WORDS = UPD_TH * UPD_STRIDE;   // one LDS mark array
+// r * UPD_STRIDE for a tile row r in [0, UPD_TH): the mask shows the compiler a 16-bit operand, so it
+// selects the full-rate v_mul_u32_u24 (r * 68 of an int of unknown range, and even __mul24 or a
+// shift-and-add it recombined, became a quarter-rate v_mul_lo_u32)
+__device__ __forceinline__ int lds_row(int r) { return (int)(((unsigned)r & 0xFFFFu) * (unsigned)UPD_STRIDE); }
 static_assert(UPD_STRIDE % 4 == 0 && UPD_STRIDE >= TILE, "quad-aligned LDS rows");
 constexpr int UPD_QUADS = TILE * UPD_TH / 4 / UPD_THREADS;  // apply quads per thread per tile
 
@@ -1828,7 +1837,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                         continue;
                     if (x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {  // bresenhamCellOcc (:266)
                         const int c = (y1 - Y0) * TILE + (x1 - X0);
-                        atomicMin(&marks[(y1 - Y0) * UPD_STRIDE + (x1 - X0)], 2u * (unsigned)b);
+                        atomicMin(&marks[lds_row(y1 - Y0) + (x1 - X0)], 2u * (unsigned)b);
                         atomicOr(&hitb[c >> 5], 1u << (c & 31));
                         anyv = 1u;
                     }
@@ -1851,8 +1860,9 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     const int s0 = bwd ? hi_i : lo_i;
                     // (s0, db, q, da < 2^15 and the tile offsets < 2^7: 24-bit multiplies throughout)
                     const unsigned num = (unsigned)w.e0 + __umul24((unsigned)s0, (unsigned)w.db);
-                    const int q = (int)udiv_small(num, (unsigned)w.da);
-                    const int err = (int)(num - __umul24((unsigned)q, (unsigned)w.da));
+                    unsigned rem;
+                    const int q = (int)udiv_small(num, (unsigned)w.da, rem);
+                    const int err = (int)rem;
                     const unsigned ev = 2u * (unsigned)b + 1u;
                     // LDS index of step s0 and its increments along the major / minor axis
                     const int la = w.x_major ? 1 : UPD_STRIDE;
@@ -1864,7 +1874,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     // (LDS addresses < 2^18, f < da < 2^13): the subtraction of db << 18 borrows exactly when
                     // f < db -- the minor axis steps -- and one select + add then moves both fields.  Three
                     // VALU per step plus the address mask, instead of five.
-                    const int dab1 = w.sa * la * 4, dab21 = dab1 + w.sb * lb * 4;
+                    const int dab1 = w.sa > 0 ? 4 * la : -4 * la;              // (no quarter-rate 32-bit multiply)
+                    const int dab21 = dab1 + (w.sb > 0 ? 4 * lb : -4 * lb);
                     const int dab = bwd ? -dab1 : dab1, dab2 = bwd ? -dab21 : dab21;
                     const int fw0 = bwd ? err : w.da - 1 - err;
                     const unsigned vdn = (unsigned)w.db << 18;
@@ -1898,20 +1909,24 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             }
             if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);
         }
+        // every pending load first (only LDS work came after them): with the loads conditional the compiler
+        // cannot count them and would otherwise wait on each quad's stores before the next.  Waited for on
+        // every iteration, with or without a pending tile (then only old stores remain, long drained): the
+        // compiler then knows no load into ql is outstanding past this point, and the next tile's address
+        // arithmetic in those registers needs no wait -- conditional, it cost a vmcnt(0) at the next loads,
+        // i.e. a wait for all of this apply's stores.
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         if (pend_tl) {
             // apply the previous tile: log-odds of every marked cell, both planes written (see below);
             // the updateIndex plane is never read --
             // a cell's stored index always predates this scan's marks (currUpdateIndex += 3 per scan)
             int *tu = reinterpret_cast<int *>(pend_tl + TILE_CELLS);
-            // every pending load first (only LDS work came after them): with the loads conditional the
-            // compiler cannot count them and would otherwise wait on each quad's stores before the next
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll
             for (int j = 0; j < UPD_QUADS; ++j) {
                 const unsigned mb = qb[j];
                 if (!(mb & 15u)) continue;
                 const int qi = tid + j * UPD_THREADS;
-                const int o = upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
+                const unsigned o = (unsigned)upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
@@ -1938,9 +1953,14 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 } else {
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        if ((mb >> c) & 1u) tu[o + c] = uv[c];
+                        if ((mb >> c) & 1u) tu[o + (unsigned)c] = uv[c];
                 }
                 touched += __popc(mb & 15u);
+                // the loaded quad stays live until its stores are issued, so the new values (nv) get
+                // registers of their own: the next tile's load into ql[j] then does not overwrite the data
+                // registers of a store still in flight -- which costs an s_waitcnt vmcnt(0), a wait for every
+                // store of this apply to complete, at the load
+                asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
             }
             pend_tl = nullptr;
         }
@@ -1950,21 +1970,29 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 // thread owns quads q = tid + j * 256 (16 quads per 64-cell row); cells outside the map
                 // (padding of edge tiles) never carry marks
                 pend_tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
+                // quad indices from an opaque copy of tid, recomputed per tile: hoisted, the second quad's
+                // load address became a 64-bit VGPR pair computed into the load's own destination registers,
+                // and that VALU write waited (vmcnt(0)) for the first quad's load -- its whole latency
+                int ot = tid;
+                asm volatile("" : "+v"(ot));
 #pragma unroll
                 for (int j = 0; j < UPD_QUADS; ++j) {
-                    const int qi = tid + j * UPD_THREADS;
-                    const int row = qi >> 4, c4 = (qi & 15) << 2;
-                    const uint4 m = *reinterpret_cast<const uint4 *>(&marks[row * UPD_STRIDE + c4]);
+                    const unsigned qi = (unsigned)ot + j * UPD_THREADS;
+                    const int row = (int)(qi >> 4), c4 = (int)((qi & 15u) << 2);
+                    const int mw = lds_row(row) + c4;
+                    const uint4 m = *reinterpret_cast<const uint4 *>(&marks[mw]);
                     const unsigned h = (hitb[row * (TILE / 32) + (c4 >> 5)] >> (c4 & 31)) & 15u;
                     const unsigned mk = (unsigned)(m.x != W_NONE) | ((unsigned)(m.y != W_NONE) << 1) |
                                         ((unsigned)(m.z != W_NONE) << 2) | ((unsigned)(m.w != W_NONE) << 3);
                     const unsigned od = (m.x & 1u) | ((m.y & 1u) << 1) | ((m.z & 1u) << 2) | ((m.w & 1u) << 3);
                     qb[j] = mk | ((od & mk) << 4) | ((h & mk) << 8);
-                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(&pend_tl[upd_off(row, c4, g.tiles_x)]);
+                    // unsigned 32-bit offset: the load takes the scalar-base + VGPR-offset form, so nothing but
+                    // the load itself writes its destination registers
+                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));
                     // restore: the quad's event words (read by this thread only) and, by the first of
                     // the 8 lanes sharing it, the hit-bit word (its readers are this wave's lanes, whose
                     // read above precedes this write)
-                    if (mk) *reinterpret_cast<uint4 *>(&marks[row * UPD_STRIDE + c4]) = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
+                    if (mk) *reinterpret_cast<uint4 *>(&marks[mw]) = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
                     if ((tid & 7) == 0) hitb[row * (TILE / 32) + (c4 >> 5)] = 0u;
                 }
             }

@@ -22,13 +22,15 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   frozen     WRONG RESULTS  hs_match_kernel runs no Gauss-Newton iteration (pose = hint): the rays no longer depend
                             on the map, so an update-kernel pricing variant built as frozen__<variant> and timed
                             against frozen alone is not confounded by a drifting match
+  notiles    WRONG RESULTS  hs_update_kernel returns after building the rays and fan boxes (prices the tile loop)
+  clk        same results   hs_update_kernel accumulates per-wave clock64() cycles of its tile-loop phases into
+                            the stream counters (gn_points: raster, updates: pending apply, steps: barrier wait,
+                            touched: mark read) -- counters() then reads the phase split, tools/clk_update.py
   noapplymath WRONG RESULTS hs_update_kernel's apply stores l + lf for every marked cell (prices the cell math)
   fullstore  WRONG RESULTS  hs_update_kernel stores whole updateIndex quads (prices the per-cell partial stores)
   ktnoswar   WRONG RESULTS  kt_addscans_kernel dword render writes the kernel bytes without the byte max
   ktnomerge  WRONG RESULTS  kt_build_kernel skips the 64-bit CAS merge of its tile into the match grid
   ktstore    WRONG RESULTS  kt_build_kernel merges with plain stores instead of compare-and-swap
-  prio1      same results   hs_match_kernel's chain wave at s_setprio 3 while it extends the sequential sums
-  prio2      same results   prio1, and the step tail (solve, sin / cos) at s_setprio 3 too
   phase1     same results   hs_match_kernel: workgroups with block id bit 8 set start ~3.6 us late (s_sleep): are
                             the co-resident workgroups' GN steps in lockstep?
   phase2     same results   the same, ~7 us
@@ -78,14 +80,6 @@ PATCHES = {
                    "    if (nw > 0) return true;\n    for (int t0 = lane; t0 < nw; t0 += 64 * 8) {\n        unsigned long long want[8], old[8];")],
     "ktstore": [("karto_kernels.hip", "                old[u] = atomicCAS(gw + wbase + r * wsw + q, 0ull, want[u]);",
                  "                gw[wbase + r * wsw + q] = want[u];")],
-    "prio1": [(K, "    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);",
-               "    if ((tid >> 6) == cw) {\n        __builtin_amdgcn_s_setprio(3);\n        if (lane < 9) run = seq_chain(T, lane, cnt, run);\n"
-               "        __builtin_amdgcn_s_setprio(0);\n    }")],
-    "prio2": [(K, "    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);",
-               "    if ((tid >> 6) == cw) {\n        __builtin_amdgcn_s_setprio(3);\n        if (lane < 9) run = seq_chain(T, lane, cnt, run);\n"
-               "    }"),
-              (K, "            sp[14] = clamp;\n        }\n    }\n    __syncthreads();",
-               "            sp[14] = clamp;\n        }\n        __builtin_amdgcn_s_setprio(0);\n    }\n    __syncthreads();")],
     "phase1": [(K, "    load_exptab();\n    __syncthreads();\n    const float *scells",
                 "    if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_sleep(127);\n    load_exptab();\n    __syncthreads();\n    const float *scells")],
     "phase2": [(K, "    load_exptab();\n    __syncthreads();\n    const float *scells",
@@ -94,8 +88,8 @@ PATCHES = {
     "noorigin": [(K, "                    if ((int)!met | (int)(lo_i > hi_i)) continue;\n",
                   "                    if (lo_i < 8) lo_i = 8;\n                    if (!met | (lo_i > hi_i)) continue;\n")],
     "nohitbit": [(K, "                    atomicOr(&hitb[c >> 5], 1u << (c & 31));\n", "                    (void)c;\n")],
-    "seqnochain": [(K, "    if ((tid >> 6) == cw && lane < 9) run = seq_chain(T, lane, cnt, run);",
-                    "    if ((tid >> 6) == cw && lane < 9) run = run + T[lane * SEQ_STRIDE];")],
+    "seqnochain": [(K, "        if (lane < 9) run = seq_chain(T, lane, cnt, run);",
+                    "        if (lane < 9) run = run + T[lane * SEQ_STRIDE];")],
     "seq4acc": [(K, "#define S2D_ADD4(v) do { run = run + (v).x; run = run + (v).y; run = run + (v).z; run = run + (v).w; } while (0)",
                  "#define S2D_ADD4(v) do { run = run + (v).x; r1 = r1 + (v).y; r2 = r2 + (v).z; r3 = r3 + (v).w; } while (0)"),
                 (K, "    const float4 *row = reinterpret_cast<const float4 *>(T + lane * SEQ_STRIDE);\n    const int c4 = cnt >> 2;",
@@ -104,10 +98,31 @@ PATCHES = {
                  "    for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];\n    return run + (r1 + (r2 + r3));")],
     "frozen": [(K, "            for (int it = 0; it <= iters; ++it) {\n                if (in_regs) {",
                 "            for (int it = 0; it <= iters && false; ++it) {\n                if (in_regs) {")],
-    "noapplymath": [(K, "                    nv[c] = ((mb >> c) & 1u) ? apply_cell(lv[c], (mb >> (4 + c)) & 1u, (mb >> (8 + c)) & 1u, lf, lo)\n                                             : lv[c];",
-                     "                    nv[c] = lv[c] + lf;")],
+    "noapplymath": [(K, "                    nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);",
+                     "                    nv[c] = t;")],
     "fullstore": [(K, "                if ((mb & 15u) == 15u) {\n                    *reinterpret_cast<int4 *>(&tu[o])",
                    "                if (true) {\n                    *reinterpret_cast<int4 *>(&tu[o])")],
+    "notiles": [(K, "    if (!__syncthreads_or(R != 0)) return;  // no ray drawn on this level\n",
+                 "    if (!__syncthreads_or(R != 0) || true) return;  // no ray drawn on this level\n")],
+    "clk": [(K, "    float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)\n",
+             "    float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)\n"
+             "    unsigned long long acc_r = 0, acc_a = 0, acc_b = 0, acc_m = 0;\n"),
+            (K, "    for (int i = 0; i <= my_tiles; ++i) {\n        const int t = part + i * parts;\n",
+             "    for (int i = 0; i <= my_tiles; ++i) {\n        const unsigned long long ck0 = clock64();\n        const int t = part + i * parts;\n"),
+            (K, "            if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);\n        }\n",
+             "            if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);\n        }\n"
+             "        const unsigned long long ck1 = clock64();\n"),
+            (K, "            pend_tl = nullptr;\n        }\n",
+             "            pend_tl = nullptr;\n        }\n        const unsigned long long ck2 = clock64();\n"
+             "        unsigned long long ck3 = ck2;\n"),
+            (K, "            lds_barrier();  // tile i's marks complete\n",
+             "            lds_barrier();  // tile i's marks complete\n            ck3 = clock64();\n"),
+            (K, "                    if ((tid & 7) == 0) hitb[row * (TILE / 32) + (c4 >> 5)] = 0u;\n                }\n            }\n        }\n    }\n",
+             "                    if ((tid & 7) == 0) hitb[row * (TILE / 32) + (c4 >> 5)] = 0u;\n                }\n            }\n        }\n"
+             "        const unsigned long long ck4 = clock64();\n"
+             "        acc_r += ck1 - ck0; acc_a += ck2 - ck1; acc_b += ck3 - ck2; acc_m += ck4 - ck3;\n    }\n"
+             "    if (lane == 0) {\n        atomicAdd(&state[s].tot_gn_points, acc_r); atomicAdd(&state[s].tot_updates, acc_a);\n"
+             "        atomicAdd(&state[s].tot_steps, acc_b); atomicAdd(&state[s].tot_touched, acc_m);\n    }\n")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

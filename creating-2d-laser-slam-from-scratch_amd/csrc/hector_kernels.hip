@@ -1956,11 +1956,6 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                         if ((mb >> c) & 1u) tu[o + (unsigned)c] = uv[c];
                 }
                 touched += __popc(mb & 15u);
-                // the loaded quad stays live until its stores are issued, so the new values (nv) get
-                // registers of their own: the next tile's load into ql[j] then does not overwrite the data
-                // registers of a store still in flight -- which costs an s_waitcnt vmcnt(0), a wait for every
-                // store of this apply to complete, at the load
-                asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
             }
             pend_tl = nullptr;
         }
@@ -1970,14 +1965,9 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 // thread owns quads q = tid + j * 256 (16 quads per 64-cell row); cells outside the map
                 // (padding of edge tiles) never carry marks
                 pend_tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
-                // quad indices from an opaque copy of tid, recomputed per tile: hoisted, the second quad's
-                // load address became a 64-bit VGPR pair computed into the load's own destination registers,
-                // and that VALU write waited (vmcnt(0)) for the first quad's load -- its whole latency
-                int ot = tid;
-                asm volatile("" : "+v"(ot));
 #pragma unroll
                 for (int j = 0; j < UPD_QUADS; ++j) {
-                    const unsigned qi = (unsigned)ot + j * UPD_THREADS;
+                    const unsigned qi = (unsigned)tid + j * UPD_THREADS;
                     const int row = (int)(qi >> 4), c4 = (int)((qi & 15u) << 2);
                     const int mw = lds_row(row) + c4;
                     const uint4 m = *reinterpret_cast<const uint4 *>(&marks[mw]);

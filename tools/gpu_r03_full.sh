@@ -1,6 +1,6 @@
 # round 3 evidence: the whole -m gpu suite, then every bench config once (CPU baselines included)
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r03m; mkdir -p $O; cd $R
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r03n; mkdir -p $O; cd $R
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
     > $O/pytest_all.log 2>&1 || { echo "FAIL gpu tests"; tail -40 $O/pytest_all.log; exit 1; }
 echo "gpu tests ok: $(tail -1 $O/pytest_all.log)"

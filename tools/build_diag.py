@@ -42,6 +42,13 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
                             32-cell half-row words (round 3), i.e. the atomicOr is not what this variant saves
   seqnochain WRONG RESULTS  hs_match_kernel's sequential sum adds one term per chunk (prices the chain adds;
                             the chunk hand-offs and barriers stay)
+  mclk       same results   hs_match_kernel accumulates the chain wave's clock64() cycles per phase of each
+                            reference-order Gauss-Newton step into the stream counters (steps: inside seq_chain,
+                            gn_points: transform + gathers + miss conversion, touched: the chunk loop, rays: step
+                            tail + its barrier, cells: the ingest prologue, updates: the level loop) -- tools/clk_match.py
+  chainregs  WRONG RESULTS  hs_match_kernel's chain reads its first 16 terms from LDS and then re-adds the
+                            registers it holds (same adds, no further LDS reads: prices the chain's LDS latency)
+  noprio     same results   hs_match_kernel's chain wave stays at the default wave priority
   seq4acc    WRONG RESULTS  hs_match_kernel's sequential sum in 4 interleaved accumulators (same instruction
                             count, a quarter of the dependency depth: latency vs issue)
 """
@@ -123,6 +130,46 @@ PATCHES = {
              "        acc_r += ck1 - ck0; acc_a += ck2 - ck1; acc_b += ck3 - ck2; acc_m += ck4 - ck3;\n    }\n"
              "    if (lane == 0) {\n        atomicAdd(&state[s].tot_gn_points, acc_r); atomicAdd(&state[s].tot_updates, acc_a);\n"
              "        atomicAdd(&state[s].tot_steps, acc_b); atomicAdd(&state[s].tot_touched, acc_m);\n    }\n")],
+    "mclk": [(K, "__device__ __forceinline__ void lds_barrier()\n",
+              "__shared__ unsigned long long s_mclk[8];\n__device__ __forceinline__ void lds_barrier()\n"),
+             (K, "        __builtin_amdgcn_s_setprio(3);\n        if (lane < 9) run = seq_chain(T, lane, cnt, run);\n",
+              "        __builtin_amdgcn_s_setprio(3);\n        __builtin_amdgcn_sched_barrier(0);\n"
+              "        const unsigned long long q0 = clock64();\n        __builtin_amdgcn_sched_barrier(0);\n"
+              "        if (lane < 9) run = seq_chain(T, lane, cnt, run);\n        __builtin_amdgcn_sched_barrier(0);\n"
+              "        const unsigned long long q1 = clock64();\n        __builtin_amdgcn_sched_barrier(0);\n"
+              "        if (lane == 0) s_mclk[0] += q1 - q0;\n"),
+             (K, "    const int tid = threadIdx.x;\n    PointFetch pf[NP];\n",
+              "    const int tid = threadIdx.x;\n    const unsigned long long mk0 = clock64();\n    PointFetch pf[NP];\n"),
+             (K, "    float run = 0.0f;                                       // SEQ: lane k < 9 of wave cw: sum of term k\n",
+              "    float run = 0.0f;                                       // SEQ: lane k < 9 of wave cw: sum of term k\n"
+              "    __builtin_amdgcn_sched_barrier(0);\n    const unsigned long long mk1 = clock64();\n    __builtin_amdgcn_sched_barrier(0);\n"),
+             (K, "    float *sp = s_pose[parity];\n    if (wave == cw) {\n",
+              "    __builtin_amdgcn_sched_barrier(0);\n    const unsigned long long mk2 = clock64();\n    __builtin_amdgcn_sched_barrier(0);\n"
+              "    float *sp = s_pose[parity];\n    if (wave == cw) {\n"),
+             (K, "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n",
+              "    __syncthreads();\n    {\n        const unsigned long long mk3 = clock64();\n"
+              "        if (SEQ && wave == cw && (tid & 63) == 0) { s_mclk[1] += mk1 - mk0; s_mclk[2] += mk2 - mk1; s_mclk[3] += mk3 - mk2; }\n"
+              "    }\n"
+              "    est[0] = sp[0];\n    est[1] = sp[1];\n"),
+             (K, "    load_exptab();\n    __syncthreads();\n    const float *scells",
+              "    const unsigned long long kk0 = clock64();\n    load_exptab();\n    if (threadIdx.x < 8) s_mclk[threadIdx.x] = 0;\n    __syncthreads();\n    const float *scells"),
+             (K, "        for (int lvl = geom.levels - 1; lvl >= 0; --lvl) {\n            const LevelGeom &g = geom.lv[lvl];\n            const int iters",
+              "        const unsigned long long kk1 = clock64();\n        if (threadIdx.x == 0) s_mclk[5] = kk1 - kk0;\n"
+              "        for (int lvl = geom.levels - 1; lvl >= 0; --lvl) {\n            const LevelGeom &g = geom.lv[lvl];\n            const int iters"),
+             (K, "        np_[0] = tmp[0];\n        np_[1] = tmp[1];\n        np_[2] = tmp[2];\n    }\n",
+              "        np_[0] = tmp[0];\n        np_[1] = tmp[1];\n        np_[2] = tmp[2];\n"
+              "        if (threadIdx.x == 0) s_mclk[6] = clock64() - kk1;\n    }\n"),
+             (K, "    if (threadIdx.x != 0) return;\n    if (local == 0) {",
+              "    __syncthreads();\n    if (threadIdx.x != 0) return;\n    if (local == 0) {"),
+             (K, "    st.tot_steps += 1;\n",
+              "    st.tot_steps += s_mclk[0];\n    st.tot_cells += s_mclk[5];\n    st.tot_rays += s_mclk[3];\n    st.tot_touched += s_mclk[2];\n"
+              "    st.tot_updates += s_mclk[6];\n"),
+             (K, "        st.tot_gn_points += it * (unsigned long long)n;\n", "        st.tot_gn_points += s_mclk[1];\n")],
+    "chainregs": [(K, "            b0 = row[i]; b1 = row[i + 1]; b2 = row[i + 2]; b3 = row[i + 3];\n",
+                   "            b0 = a0; b1 = a1; b2 = a2; b3 = a3;\n"),
+                  (K, "            a0 = row[i + 4]; a1 = row[i + 5]; a2 = row[i + 6]; a3 = row[i + 7];\n", "")],
+    "noprio": [(K, "        // it issues ahead of the co-resident workgroups' waves (s_setprio; back to 0 after the step tail)\n        __builtin_amdgcn_s_setprio(3);\n",
+                "        // it issues ahead of the co-resident workgroups' waves (s_setprio; back to 0 after the step tail)\n        __builtin_amdgcn_s_setprio(0);\n")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

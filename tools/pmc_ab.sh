@@ -16,13 +16,13 @@ for v in "$@"; do
     SLAM2D_LIB=$lib timeout -k 10 120 rocprofv3 --pmc $set -d "$OUT/p$i" -o run --output-format csv -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-copy-probe --steps 5 --warmup 2 > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   done
   python3 - "$OUT" "$v" <<'PY'
-import csv, glob, sys, collections
+import csv, glob, os, sys, collections
 agg = collections.defaultdict(float); cnt = collections.Counter()
 for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("s2d::", "")
+        k = r["Kernel_Name"].split("(")[0].replace("s2d::", "").replace("void ", "")
         agg[(k, r["Counter_Name"])] += float(r["Counter_Value"]); cnt[(k, r["Counter_Name"])] += 1
 for (k, c), v in sorted(agg.items()):
-    if k.startswith("hs_update"): print(sys.argv[2], f"{k:18s} {c:24s} {v/ max(cnt[(k,c)],1):16.0f}")
+    if k.startswith(os.environ.get("KPREFIX", "hs_update")): print(sys.argv[2], f"{k:18s} {c:24s} {v/ max(cnt[(k,c)],1):16.0f}")
 PY
 done

@@ -714,8 +714,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one rank per GPU over RCCL (the driver's node).  BENCH_DIST_BACKEND=gloo rehearses the N > 1 path
+        # with several ranks on one GPU (RCCL refuses two ranks on one device): timing collectives on gloo
+        dev_idx = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev_idx)
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())

@@ -49,6 +49,8 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   chainregs  WRONG RESULTS  hs_match_kernel's chain reads its first 16 terms from LDS and then re-adds the
                             registers it holds (same adds, no further LDS reads: prices the chain's LDS latency)
   noprio     same results   hs_match_kernel's chain wave stays at the default wave priority
+  dwordq     same results   hs_update_kernel loads and stores only the marked cells of a partially marked quad
+                            (4-byte accesses; whole quads stay 16-byte): prices the over-fetch of partial quads
   seq4acc    WRONG RESULTS  hs_match_kernel's sequential sum in 4 interleaved accumulators (same instruction
                             count, a quarter of the dependency depth: latency vs issue)
 """
@@ -170,6 +172,17 @@ PATCHES = {
                   (K, "            a0 = row[i + 4]; a1 = row[i + 5]; a2 = row[i + 6]; a3 = row[i + 7];\n", "")],
     "noprio": [(K, "        // it issues ahead of the co-resident workgroups' waves (s_setprio; back to 0 after the step tail)\n        __builtin_amdgcn_s_setprio(3);\n",
                 "        // it issues ahead of the co-resident workgroups' waves (s_setprio; back to 0 after the step tail)\n        __builtin_amdgcn_s_setprio(0);\n")],
+    "dwordq": [(K, "                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));\n",
+                "                    if (mk == 15u) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));\n"
+                "                    else if (mk) {\n"
+                "                        const float *qp = pend_tl + (unsigned)upd_off(row, c4, g.tiles_x);\n"
+                "                        if (mk & 1u) ql[j].x = qp[0];\n                        if (mk & 2u) ql[j].y = qp[1];\n"
+                "                        if (mk & 4u) ql[j].z = qp[2];\n                        if (mk & 8u) ql[j].w = qp[3];\n"
+                "                    }\n"),
+               (K, "                *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);\n",
+                "                if ((mb & 15u) == 15u) *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);\n"
+                "                else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n"
+                "                        if ((mb >> c) & 1u) pend_tl[o + (unsigned)c] = nv[c];\n                }\n")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

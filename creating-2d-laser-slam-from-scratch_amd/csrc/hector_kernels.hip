@@ -1812,12 +1812,20 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                               (int)(gb.y < Y1));
             }
             {
-                for (int b0 = wave_beam0; (b0 & ~255) < n; b0 += UPD_THREADS) {
-                    const int fi = b0 >> 6;  // wave-uniform
-                    if (fi < 64) {
-                        if (!((fm >> fi) & 1ull)) continue;
+                // this wave's groups (fi = wave + 4 k) among the first 64 that meet the tile, one set bit each:
+                // the loop visits only those (scalar find-first-set), then the groups past 64 test their box
+                unsigned long long gm = fm & (0x1111111111111111ull << (wave_beam0 >> 6));
+                int b0x = wave_beam0 + 64 * 64;  // groups >= 64 (scans of > 4096 points)
+                for (;;) {
+                    int b0;
+                    if (gm) {
+                        b0 = __builtin_ctzll(gm) << 6;
+                        gm &= gm - 1ull;
                     } else {
-                        const int4 gb = gbox[fi];
+                        if ((b0x & ~255) >= n) break;
+                        b0 = b0x;
+                        b0x += UPD_THREADS;
+                        const int4 gb = gbox[b0 >> 6];
                         const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
                         const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
                         if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;

@@ -1790,9 +1790,17 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     float4 ql[UPD_QUADS];      // pending tile: log-odds of the marked quads (loads in flight)
     unsigned qb[UPD_QUADS];    // pending tile: 12 mark bits per quad (see apply_cell)
     float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)
-    for (int i = 0; i <= my_tiles; ++i) {
-        const int t = part + i * parts;
-        const int ty = ty0 + t / ntx, tx = tx0 + t % ntx;
+    // tile t = part + i * parts of the box (row-major): its column and row are carried from tile to tile
+    // (a division of t by the box width per tile was ~20 scalar instructions of signed-division code)
+    int tcol = part % ntx, trow = part / ntx;
+    for (int ii = 0; ii <= my_tiles; ++ii) {
+        const int i = __builtin_amdgcn_readfirstlane(ii);  // uniform (the compiler had put it in a VGPR)
+        const int ty = ty0 + trow, tx = tx0 + tcol;
+        tcol += parts;
+        while (tcol >= ntx) {
+            tcol -= ntx;
+            ++trow;
+        }
         const int X0 = tx * TILE, Y0 = ty * UPD_TH;
         const int X1 = X0 + TILE, Y1 = Y0 + UPD_TH;
         const int buf = i & 1;

@@ -51,6 +51,8 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
   noprio     same results   hs_match_kernel's chain wave stays at the default wave priority
   dwordq     same results   hs_update_kernel loads and stores only the marked cells of a partially marked quad
                             (4-byte accesses; whole quads stay 16-byte): prices the over-fetch of partial quads
+  mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
+                            streams per CU)
   seq4acc    WRONG RESULTS  hs_match_kernel's sequential sum in 4 interleaved accumulators (same instruction
                             count, a quarter of the dependency depth: latency vs issue)
 """
@@ -183,6 +185,9 @@ PATCHES = {
                 "                if ((mb & 15u) == 15u) *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);\n"
                 "                else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n"
                 "                        if ((mb >> c) & 1u) pend_tl[o + (unsigned)c] = nv[c];\n                }\n")],
+    "mlds3": [(K, "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n",
+               "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n"
+               "    __shared__ float s_pad[3000];\n    if (stream_begin < 0) s_pad[threadIdx.x] = 1.0f;\n")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

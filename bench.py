@@ -62,6 +62,12 @@ def kernel_source_id() -> str:
     return h.hexdigest()[:16]
 
 
+def issue_split() -> str:
+    """How a step is issued (part of the PMC workload key: launches per step and streams per launch differ)."""
+    return (f"pipeline={os.environ.get('SLAM2D_PIPELINE', '0') or '0'},parts={os.environ.get('SLAM2D_PARTS', '1') or '1'},"
+            f"update={os.environ.get('SLAM2D_UPDATE', 'single') or 'single'}")
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -275,6 +281,26 @@ def pose_check(cfg, S, gpu_poses, streams, thresholds=(-1.0, -1.0), order=0):
             "vs_oracle_in_kernel_order_exact_frac": float((np.abs(etree).max(axis=1) == 0.0).mean()),
             "vs_ground_truth_rmse_xy_m": float(np.sqrt(np.mean(egt[:, 0] ** 2 + egt[:, 1] ** 2))),
             "vs_ground_truth_rmse_theta_rad": float(np.sqrt(np.mean(egt[:, 2] ** 2)))}
+
+
+def north_star_targets(value, cpu, roof, pose):
+    """BASELINE.json north_star's targets, each with its measured value and pass/fail: >= 100x the
+    reference CPU path on 1 GPU (against one core, and against all the box's cores used here), >= 40 % of
+    the HBM-read roofline (SURVEY 8d's read model and the counted reads), pose error <= 1e-4 m / rad."""
+    def row(v, target, op, **kw):
+        return {"value": None if v is None else round(v, 5), "target": target, "op": op,
+                "pass": None if v is None else bool(v >= target if op == ">=" else v <= target), **kw}
+    allc = (cpu or {}).get("all_cores")
+    return {"x_cpu_1core": row(value / cpu["value"] if cpu else None, 100.0, ">=", cores=1,
+                               basis=(cpu or {}).get("kind")),
+            "x_cpu_all_cores": row(value / allc["value"] if allc else None, 100.0, ">=",
+                                   cores=allc["cores"] if allc else None, basis="port" if allc else None),
+            "read_roofline_model": row((roof or {}).get("read_only_frac"), 0.40, ">=",
+                                       basis="SURVEY 8d read bytes (match gathers + 8 B per cell touch) / step wall time"),
+            "read_roofline_counted": row((roof or {}).get("read_only_frac_counters"), 0.40, ">=",
+                                         basis="rocprofv3 FETCH_SIZE x 2 of the step's kernels / step wall time"),
+            "pose_error_m": row(pose["max_abs_xy_m"], 1e-4, "<=", basis="max |GPU - oracle (reference order)|"),
+            "pose_error_rad": row(pose["max_abs_theta_rad"], 1e-4, "<=", basis="max |GPU - oracle (reference order)|")}
 
 
 GM_METRIC = "particle-scans/sec (1081-beam) GMapping ComputeMap, particles sharded over GPUs"
@@ -672,6 +698,52 @@ def run_karto(args, world, rank, dev):
         dist.destroy_process_group()
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) without an external launcher: start N ranks, one process per GPU, as
+    `python -m torch.distributed.run --nproc-per-node N bench.py <same args>` on 127.0.0.1 (a child
+    process -- this parent makes no HIP / torch.cuda call and never execs), relay rank 0's JSON line and
+    return the launcher's exit code (non-zero when any rank failed)."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    print(f"[bench] launching {n} ranks: {' '.join(cmd[2:])}", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for ln in p.stdout:  # only rank 0 prints to stdout (one JSON line); anything else goes to stderr
+        if ln.startswith("{"):
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(ln)
+    return p.wait()
+
+
+def launcher_selftest(args):
+    """Rank body of the launcher's CPU test (no GPU): gloo all-reduce of every rank's unit count, rank 0
+    prints the job's line as the benchmarks do."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    t_max, total = aggregate_over_ranks(time.perf_counter() - t0 + 1e-3, float(args.streams or 1), torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"metric": "launcher-selftest", "value": total / t_max, "unit": "units/s", "n_gpus": world,
+                          "config": {"global_batch": int(total), "ranks": world}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -705,7 +777,20 @@ def main():
     ap.add_argument("--input", choices=["ranges", "points"], default="ranges",
                     help="hector: raw LaserScan ranges through the on-device ingest (scanCallback, default) or "
                          "pre-converted DataContainer points")
+    ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    # --gpus N: the driver launches N > 1 ranks with torch.distributed.run (WORLD_SIZE set, = N); a bare
+    # `bench.py --gpus N` starts them itself (launch_ranks) before anything touches the GPU
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args.gpus)
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}: refusing a mislabelled run",
+              file=sys.stderr, flush=True)
+        return 2
+    if args.launcher_selftest:
+        return launcher_selftest(args)
 
     import torch
     import torch.distributed as dist
@@ -767,7 +852,7 @@ def main():
         fleet.set_reduction_order(HectorFleet.ORDER_TREE256)
     order = fleet.reduction_order()
     workload = {"config": args.config, "streams": B, "semantics": args.semantics, "order": order,
-                "kernel_src": kernel_source_id()}
+                "kernel_src": kernel_source_id(), "issue_split": issue_split()}
     hs = torch.cuda.current_stream(dev).cuda_stream
     # pose log: every 64th stream and the last one (the top of the update lists and of the HBM range)
     log_streams = sorted(set(range(0, B, 64)) | {B - 1})
@@ -826,8 +911,11 @@ def main():
     # instrumented pass: the same K-step workload on the next K scans, HIP events around every kernel
     # on the stream it is launched on (the library's timing events)
     ktimes, ctr_i, elapsed_i = None, None, None
+    clk = None
     if P:
         fleet.set_timing(True)
+        fleet.set_clock_probe(True)   # effective shader clock of the instrumented pass (s_memtime / s_memrealtime)
+        fleet.clock_probe(reset=True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         if pipelined:
@@ -838,6 +926,8 @@ def main():
         torch.cuda.synchronize()
         elapsed_i = time.perf_counter() - t1
         fleet.set_timing(False)
+        clk = fleet.clock_probe(reset=True)
+        fleet.set_clock_probe(False)
         ktimes = fleet.kernel_times(reset=True)
         ctr_i = fleet.counters(reset=True)
 
@@ -888,12 +978,29 @@ def main():
                     # the north star's "HBM-read roofline": SURVEY 8d's read subset (match gathers + 8 B per cell
                     # touch) over the step's wall time, and the counted reads of the step's kernels (PMC)
                     "read_only_frac": round(ab["read_only"] / t_max / 1e9 / HBM_PEAK_GBS, 5),
-                    "read_only_frac_counters": (round((2 * pmc["fetch_kb"] + 2 * mpmc["fetch_kb"]) * 1024 * K
+                    # counted reads per launch x launches per step (ktimes over the P instrumented steps) x K
+                    "read_only_frac_counters": (round(2 * (pmc["fetch_kb"] * ktimes["update"][1] + mpmc["fetch_kb"]
+                                                           * ktimes["match"][1]) / P * 1024 * K
                                                       / t_max / 1e9 / HBM_PEAK_GBS, 5)
                                                 if (pmc and mpmc and dom == "update") else None),
                     "alg_bytes_per_scan": int(ab["total"] / max(B * K, 1)),
                     "cells_per_scan": round(ctr["cells"] / max(B * K, 1), 1),
                     "distinct_cells_per_scan": round(ctr["touched"] / max(B * K, 1), 1)}
+            if clk:
+                # effective shader clock over the instrumented pass (every 16th workgroup's lifetime): kernel
+                # times compare across boxes as cycles = ms x clock
+                ck = clk["update" if dom == "update" else "match"]
+                roof["sclk_mhz"] = ck["sclk_mhz"]
+                roof["match_sclk_mhz"] = clk["match"]["sclk_mhz"]
+                roof["update_sclk_mhz"] = clk["update"]["sclk_mhz"]
+                if ck["sclk_mhz"]:
+                    roof["mcycles_per_launch"] = round(ms / nlaunch * 1e-3 * ck["sclk_mhz"], 3)
+                roof["clock_probe"] = clk
+            for kk, ent in (("update", pmc), ("match", mpmc)):
+                # instruction counts per launch from the committed PMC summary of this workload (when taken)
+                if ent and ent.get("insts_valu") is not None:
+                    roof.setdefault("pmc_insts_per_launch", {})[kk] = {
+                        c: ent.get(c) for c in ("insts_valu", "insts_salu", "insts_lds", "wave_cycles", "busy_cycles")}
             if not args.no_copy_probe:
                 roof["attainable_copy_GBps"] = round(copy_bandwidth(dev), 1)
         cpu = None
@@ -919,10 +1026,12 @@ def main():
                                     if pipelined else "one batch call per step"),
                           "parallelism": f"replicas x{world}", "semantics": args.semantics,
                           "reduction_order": order, "kernel_src": workload["kernel_src"],
+                          "issue_split": workload["issue_split"],
                           "map_updates_per_scan": round(ctr["updates"] / max(B * K, 1), 4)},
                "roofline": roof, "cpu_baseline": cpu, "pose_vs_ref": pose}
         if cpu:
             out["speedup_vs_cpu_1core"] = round(value / cpu["value"], 1)
+        out["targets"] = north_star_targets(value, cpu, roof, pose)
         print(json.dumps(out), flush=True)
     fleet.close()
     if world > 1:
@@ -930,4 +1039,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -121,6 +121,8 @@ struct hs_ctx {
     int *d_in = nullptr;
     float2 *d_iorigo = nullptr;
     float *d_ranges1 = nullptr;
+    // clock probe buffer (hs_set_clock_probe): 8 counters, see FleetGeom::clk
+    unsigned long long *d_clk = nullptr;
 };
 
 namespace {
@@ -255,6 +257,15 @@ size_t upd_shmem_bytes(const hs_ctx *c)
     return sizeof(unsigned) * ((size_t)UPD_FIXED_WORDS + rays + UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));
 }
 
+// hs_update_kernel's packed raster walk keeps the Bresenham error f < da in 14 bits (V = f << 18 | LDS
+// address): rays of at most 16384 cells, i.e. level-0 maps of at most 16385 cells per side.  Larger maps
+// take the binned kernels (their walk keeps the error in its own register), as do scans whose rays would
+// not fit the kernel's LDS (the binned kernels' LDS use is independent of the scan size).
+bool upd_single_ok(const hs_ctx *c)
+{
+    return c->update_single && upd_shmem_bytes(c) <= 65536 && c->sx <= 16385 && c->sy <= 16385;
+}
+
 int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int xy_stride, const int *n,
                 const float2 *origo, const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s,
                 hipEvent_t wait_before_update = nullptr, const MatchIngest *mi = nullptr)
@@ -267,7 +278,7 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     // the single-kernel update consumes the match kernel's list of updating streams (wl[part][parity]: one
     // pair of lists per part)
     const size_t upd_shmem = upd_shmem_bytes(c);
-    const bool single = c->update_single && upd_shmem <= 65536;
+    const bool single = upd_single_ok(c);
     const bool use_list = single && !c->upd_parts_fixed && mode != MODE_MATCH_ONLY;
     UpdList *wl_cur = use_list ? c->wl[part][c->wl_parity[part]] : nullptr;
     begin_timed(c, 0, s);
@@ -390,8 +401,7 @@ int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride
 // The pipelined run (hs_run_ranges_device) needs the list-driven single update kernel on every part.
 bool pipeline_ok(const hs_ctx *c)
 {
-    const size_t upd_shmem = upd_shmem_bytes(c);
-    return c->pipeline && c->nq >= 2 && c->update_single && upd_shmem <= 65536 && !c->upd_parts_fixed && c->B >= 2;
+    return c->pipeline && c->nq >= 2 && upd_single_ok(c) && !c->upd_parts_fixed && c->B >= 2;
 }
 
 int check_stream(hs_ctx *c, int stream) { return (c && stream >= 0 && stream < c->B) ? HS_OK : HS_EINVAL; }
@@ -635,6 +645,7 @@ int hs_destroy(hs_ctx *c)
     hipFree(c->d_in);
     hipFree(c->d_iorigo);
     hipFree(c->d_ranges1);
+    hipFree(c->d_clk);
     for (auto &p : c->ev_used) {
         hipEventDestroy(p.a);
         hipEventDestroy(p.b);
@@ -1159,6 +1170,37 @@ int hs_get_kernel_times(hs_ctx *c, double ms_out[3], int64_t launches_out[3], in
             c->acc_n[k] = 0;
         }
     }
+    return HS_OK;
+}
+
+int hs_set_clock_probe(hs_ctx *c, int enable)
+{
+    if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    LOCK(c);
+    if (enable && !c->d_clk) {
+        HCHK(hipMalloc(&c->d_clk, 8 * sizeof(unsigned long long)));
+        HCHK(hipMemsetAsync(c->d_clk, 0, 8 * sizeof(unsigned long long), c->stream));
+        HCHK(hipStreamSynchronize(c->stream));
+    }
+    c->geom.clk = enable ? c->d_clk : nullptr;
+    return HS_OK;
+}
+
+int hs_get_clock_probe(hs_ctx *c, double out[6], int reset)
+{
+    if (!c || !out) return fail(HS_EINVAL, "NULL argument");
+    LOCK(c);
+    for (int k = 0; k < 6; ++k) out[k] = 0.0;
+    if (!c->d_clk) return HS_OK;
+    HCHK(hipDeviceSynchronize());  // the probed kernels may have run on any stream (*_device calls)
+    unsigned long long h[8];
+    HCHK(hipMemcpy(h, c->d_clk, sizeof(h), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 2; ++k) {
+        out[3 * k] = (double)h[4 * k];
+        out[3 * k + 1] = (double)h[4 * k + 1];
+        out[3 * k + 2] = (double)h[4 * k + 2];
+    }
+    if (reset) HCHK(hipMemset(c->d_clk, 0, sizeof(h)));
     return HS_OK;
 }
 

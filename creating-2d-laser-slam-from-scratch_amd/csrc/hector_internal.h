@@ -77,8 +77,12 @@ struct FleetGeom {
     size_t stream_words;       // 4-byte words per stream (all levels, tiled, both planes)
     int upd_parts[MAX_LEVELS]; // hs_update_kernel workgroups per (stream, level)
     int upd_minp[MAX_LEVELS];  // list-driven split: at least this many workgroups per level (0: upd_split's)
+    // clock probe (hs_set_clock_probe; NULL = off): [kernel * 4 + {0: shader cycles, 1: 100-MHz ticks,
+    // 2: workgroups}] summed over every CLK_SAMPLE-th workgroup's lifetime (kernel 0 match, 1 update)
+    unsigned long long *clk;
     LevelGeom lv[MAX_LEVELS];
 };
+constexpr int CLK_SAMPLE = 16;
 
 // Per-stream processor state (HectorSlamProcessor members + per-grid update indices).
 struct alignas(16) StreamState {

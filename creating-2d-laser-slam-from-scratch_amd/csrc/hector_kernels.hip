@@ -69,6 +69,30 @@ __device__ __forceinline__ bool pose_diff_larger(const float *p1, const float *p
     return fabsf(ad) > ang;
 }
 
+// Clock probe (hs_set_clock_probe): every CLK_SAMPLE-th workgroup subtracts its entry stamps and adds
+// its exit stamps -- s_memtime (shader cycles) and s_memrealtime (100-MHz constant ticks) -- so clk[4k]
+// / clk[4k + 1] x 100 MHz is the effective shader clock over the sampled lifetimes of kernel k
+// (MI355X_MICROARCH.md, in-kernel clock).  The stamps go straight to memory (vector atomics), so no
+// register is held across the kernel; with the probe off it is one uniform branch at entry and exit.
+__device__ __forceinline__ void clk_stamp(unsigned long long *clk, int kernel, bool entry)
+{
+    if (clk == nullptr || (blockIdx.x % CLK_SAMPLE) != 0 || threadIdx.x != 0) return;
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long c = __builtin_amdgcn_s_memtime();
+    const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the stamps are back before any LDS wait is counted
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long *k = clk + 4 * kernel;
+    if (entry) {
+        atomicAdd(k, 0ull - c);
+        atomicAdd(k + 1, 0ull - r);
+    } else {
+        atomicAdd(k, c);
+        atomicAdd(k + 1, r);
+        atomicAdd(k + 2, 1ull);
+    }
+}
+
 // exp's 2^(j/128) table (detmath.h): read once per workgroup into LDS by the kernels that call
 // cell_prob (hs_match_kernel, load_exptab), so the per-lane table reads are LDS reads
 __constant__ double c_exptab[SDM_EXPTAB_N] = {SDM_EXPTAB_VALUES};
@@ -724,6 +748,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     const int local = blockIdx.x;
     const int s = stream_begin + local;
     StreamState &st = state[s];
+    clk_stamp(geom.clk, 0, true);
     load_exptab();
     __syncthreads();
     const float *scells = cells + (size_t)s * geom.stream_words;
@@ -814,6 +839,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
         np_[1] = tmp[1];
         np_[2] = tmp[2];
     }
+    clk_stamp(geom.clk, 0, false);
     if (threadIdx.x != 0) return;
     if (local == 0) {  // reset the grid-update work queue for this step (consumed by k2/k3)
         wq->seg_used = 0;
@@ -1692,6 +1718,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     const int s = stream_begin + local;
     const StreamState &st = state[s];
     if (!st.do_update) return;
+    clk_stamp(geom.clk, 1, true);
     const LevelGeom &g = geom.lv[lvl];
     // level 0: this step's DataContainer; levels >= 1: the stored one of the last match
     // (MapRepMultiMap::updateByScan, MapRepMultiMap.h:181-188; equal to this step's after a match)
@@ -1764,7 +1791,10 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                                                  ? make_uint4(W_NONE, W_NONE, W_NONE, W_NONE)
                                                  : make_uint4(0u, 0u, 0u, 0u);
     if (tid < 2) s_any[tid] = 0u;
-    if (!__syncthreads_or(R != 0)) return;  // no ray drawn on this level
+    if (!__syncthreads_or(R != 0)) {  // no ray drawn on this level
+        clk_stamp(geom.clk, 1, false);
+        return;
+    }
     const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / UPD_TH;
     const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / UPD_TH;
     const int mark_free = st.mark_base + 1;  // currMarkFreeIndex (:120)
@@ -1887,7 +1917,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     const int li = __mul24(ia, la) + __mul24(ib, lb);
                     // incremental walk, f = da - 1 - error_b in [0, da) (backwards: g = error_b), packed with
                     // the LDS byte address of the step's mark word into ONE register, V = f << 18 | address
-                    // (LDS addresses < 2^18, f < da < 2^13): the subtraction of db << 18 borrows exactly when
+                    // (LDS addresses < 2^18, f < da <= 2^14: the host sends larger maps to the binned kernels,
+                    // upd_single_ok): the subtraction of db << 18 borrows exactly when
                     // f < db -- the minor axis steps -- and one select + add then moves both fields.  Three
                     // VALU per step plus the address mask, instead of five.
                     const int dab1 = w.sa > 0 ? 4 * la : -4 * la;              // (no quarter-rate 32-bit multiply)
@@ -2007,6 +2038,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);
     if (lane == 0 && touched) atomicAdd(&state[s].tot_touched, (unsigned long long)touched);
+    clk_stamp(geom.clk, 1, false);
 }
 
 // --------------------------------------------------------------------------- utility kernels

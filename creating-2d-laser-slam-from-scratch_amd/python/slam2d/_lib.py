@@ -61,6 +61,8 @@ def _declare(L):
     L.hs_get_stream.argtypes = [_p]
     L.hs_set_timing.argtypes = [_p, _i]
     L.hs_get_kernel_times.argtypes = [_p, _p, _p, _i]
+    L.hs_set_clock_probe.argtypes = [_p, _i]
+    L.hs_get_clock_probe.argtypes = [_p, _p, _i]
     L.hs_default_laser.restype = None
     L.hs_default_laser.argtypes = [_p, _i, _f, _f]
     L.hs_set_laser.argtypes = [_p, _p, _p]

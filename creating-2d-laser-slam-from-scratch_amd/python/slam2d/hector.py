@@ -303,6 +303,22 @@ class HectorFleet:
         names = ("match", "bin", "update")  # slot 2: hs_update_kernel (default) or hs_tile_kernel (binned)
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}
 
+    def set_clock_probe(self, enable: bool):
+        check(self.L.hs_set_clock_probe(self.h, 1 if enable else 0), "hs_set_clock_probe")
+
+    def clock_probe(self, reset=True):
+        """Effective shader clock (MHz) of the match and update kernels over the sampled workgroups'
+        lifetimes since the last reset (s_memtime / s_memrealtime x 100 MHz), with the raw sums."""
+        o = np.zeros(6, np.float64)
+        check(self.L.hs_get_clock_probe(self.h, _fp(o), 1 if reset else 0), "hs_get_clock_probe")
+        out = {}
+        for i, k in enumerate(("match", "update")):
+            cyc, ticks, wgs = o[3 * i: 3 * i + 3]
+            out[k] = {"sclk_mhz": round(cyc / ticks * 100.0, 1) if ticks > 0 else None,
+                      "cycles": int(cyc), "ticks_100mhz": int(ticks), "workgroups_sampled": int(wgs),
+                      "cycles_per_workgroup": round(cyc / wgs, 1) if wgs else None}
+        return out
+
 
 class HectorSlamProcessor:
     """hectorslam::HectorSlamProcessor (slam_main/HectorSlamProcessor.h:54-149), device-backed."""

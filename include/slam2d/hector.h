@@ -199,6 +199,13 @@ int hs_get_reduction_order(hs_ctx *ctx, int *order_out);
  * hs_tile_kernel}, the accumulated milliseconds and launch counts since the last reset (synchronises). */
 int hs_set_timing(hs_ctx *ctx, int enable);
 int hs_get_kernel_times(hs_ctx *ctx, double ms_out[3], int64_t launches_out[3], int reset);
+/* Effective shader clock of the Hector kernels (no reference counterpart).  With the probe on, every
+ * 16th workgroup of hs_match_kernel and hs_update_kernel adds its lifetime in shader cycles (s_memtime)
+ * and in 100-MHz real-time ticks (s_memrealtime); hs_get_clock_probe (synchronises) returns
+ * {match cycles, match ticks, match workgroups, update cycles, update ticks, update workgroups}
+ * since the last reset: clock = cycles / ticks x 100 MHz. */
+int hs_set_clock_probe(hs_ctx *ctx, int enable);
+int hs_get_clock_probe(hs_ctx *ctx, double out[6], int reset);
 
 #ifdef __cplusplus
 }

@@ -277,6 +277,31 @@ def test_degenerate_rays(gpu):
         np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))
 
 
+def test_long_rays_over_16384_cells(gpu):
+    """Rays longer than 16384 cells (a 16640 x 64 map, the robot near its left end): the default update
+    kernel's packed walk holds the Bresenham error in 14 bits, so the host sends such maps to the binned
+    kernels (upd_single_ok); the result must still equal the oracle cell for cell."""
+    sx, sy = 16640, 64
+    pts = [(821.7, 0.3), (821.7, -1.2), (700.0, 0.9), (-5.0, 0.2), (3.0, 1.0), (0.5, -1.5)]
+    pts = np.asarray(pts, np.float32)
+    fleet = HectorFleet(1, 0.05, sx, (0.01, 0.5), 2, max_points=len(pts), map_size_y=sy)
+    ora = O.HectorOracle(0.05, sx, (0.01, 0.5), 2, reduce_threads=T_RED, map_size_y=sy)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(-1.0, -1.0)
+    for k, pose in enumerate([(0.0, 0.0, 0.0), (0.5, 0.3, 0.001), (-0.2, -0.1, -0.0004)]):
+        pose = np.asarray(pose, np.float32)
+        fleet.update_by_scan(0, pts, pose)
+        ora.update_by_scan(pts, pose)
+    ctr = fleet.counters(reset=False)
+    assert ctr["cells"] > 3 * 16384, ctr  # the long rays were drawn
+    for lvl in range(2):
+        m = fleet.get_map(0, lvl)
+        ol, ou = ora.level(lvl)
+        np.testing.assert_array_equal(m["upd"], ou, err_msg=f"level {lvl}")
+        np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol), err_msg=f"level {lvl}")
+
+
 def test_reset(gpu, scans):
     """HectorSlamProcessor::reset (HectorSlamProcessor.h:111-117): grids cleared and poses reset; the grids'
     update indices (GridMapBase::reset clears cells only), the covariance and the stored containers stay

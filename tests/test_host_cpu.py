@@ -237,3 +237,52 @@ def test_rccl_unique_id_with_nul_bytes_gloo_world2():
     with pytest.raises(Exception):
         unique_id_from_bytes(raw[:1])
     assert C.sizeof(_UniqueId) == 128
+
+
+# ------------------------------------------------------------------ bench.py --gpus N launcher
+def _bench_env():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env["PYTHONPATH"] = bench.REPO
+    return env
+
+
+def test_bench_gpus_n_launches_its_ranks():
+    """`bench.py --gpus 2` with no external launcher starts 2 ranks itself (torch.distributed.run as a child
+    process) and relays rank 0's one JSON line: n_gpus 2, the global batch is both ranks' units."""
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, os.path.join(bench.REPO, "bench.py"), "--gpus", "2", "--streams", "512",
+                        "--launcher-selftest"], capture_output=True, text=True, timeout=300, env=_bench_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 1024, out
+
+
+def test_bench_world_size_mismatch_is_refused():
+    """WORLD_SIZE set by a launcher but different from --gpus: exit non-zero instead of a mislabelled line."""
+    import subprocess
+    import sys
+
+    env = _bench_env()
+    env.update({"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    r = subprocess.run([sys.executable, os.path.join(bench.REPO, "bench.py"), "--gpus", "1", "--launcher-selftest"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr, (r.returncode, r.stderr[-500:])
+
+
+def test_north_star_targets_block():
+    """The bench line's targets block: each target with its value and pass/fail."""
+    cpu = {"value": 1000.0, "kind": "port", "all_cores": {"value": 15000.0, "cores": 16}}
+    roof = {"read_only_frac": 0.48, "read_only_frac_counters": 0.12}
+    pose = {"max_abs_xy_m": 0.0, "max_abs_theta_rad": 0.0}
+    t = bench.north_star_targets(1.4e6, cpu, roof, pose)
+    assert t["x_cpu_1core"]["value"] == 1400.0 and t["x_cpu_1core"]["pass"]
+    assert t["x_cpu_all_cores"]["cores"] == 16 and round(t["x_cpu_all_cores"]["value"], 2) == 93.33
+    assert not t["x_cpu_all_cores"]["pass"]
+    assert t["read_roofline_model"]["pass"] and not t["read_roofline_counted"]["pass"]
+    assert t["pose_error_m"]["pass"] and t["pose_error_rad"]["pass"]
+    assert bench.north_star_targets(1.0, None, None, pose)["x_cpu_1core"]["pass"] is None

@@ -22,6 +22,9 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+INSTS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVES")
+
+
 def short(name: str) -> str:
     return name.split("(")[0].replace("void ", "").replace("s2d::", "")
 
@@ -41,7 +44,8 @@ def main():
                     if k in bench["config"]), None)
     # the workload key bench.py matches on (Hector lines carry semantics and summation order)
     wkey = {"config": cfg, "streams": streams}
-    for k, field in (("semantics", "semantics"), ("order", "reduction_order"), ("kernel_src", "kernel_src")):
+    for k, field in (("semantics", "semantics"), ("order", "reduction_order"), ("kernel_src", "kernel_src"),
+                     ("issue_split", "issue_split")):
         if field in bench["config"]:
             wkey[k] = bench["config"][field]
 
@@ -50,30 +54,44 @@ def main():
         for r in csv.DictReader(f):
             dur[short(r["Name"])] = (int(r["Calls"]), float(r["AverageNs"]))
     pmc = collections.defaultdict(dict)
-    for sub, ctr in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+    # the instruction pass (SQ_INSTS_*, SQ_*_CYCLES) is optional: summaries of earlier rounds have none
+    passes = [("pmc_fetch", ("FETCH_SIZE",)), ("pmc_write", ("WRITE_SIZE",)), ("pmc_insts", INSTS)]
+    for sub, ctrs in passes:
+        path = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(path) and sub == "pmc_insts":
+            continue
         acc = collections.defaultdict(list)
-        with open(os.path.join(src, sub, "run_counter_collection.csv")) as f:
+        with open(path) as f:
             for r in csv.DictReader(f):
-                if r["Counter_Name"] == ctr:
-                    acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-        for k, v in acc.items():
+                if r["Counter_Name"] in ctrs:
+                    acc[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+        for (k, ctr), v in acc.items():
             pmc[k][ctr] = sum(v) / len(v)
 
     lines = [f"# rocprofv3 summary `{tag}` ({cfg}, {streams} units/GPU)", "",
              f"bench line of the traced run: value {bench['value']} {bench['unit']}, ms/step {bench['ms_per_step']}", "",
-             "| kernel | calls | avg us | FETCH_SIZE KB | WRITE_SIZE KB | HBM bytes/launch (2F+W) | GB/s |",
-             "|---|---|---|---|---|---|---|"]
+             "| kernel | calls | avg us | FETCH_SIZE KB | WRITE_SIZE KB | HBM bytes/launch (2F+W) | GB/s "
+             "| VALU insts | SALU insts | LDS insts | wave cycles |",
+             "|---|---|---|---|---|---|---|---|---|---|---|"]
     entries = []
     for k, (calls, avg) in sorted(dur.items(), key=lambda kv: -kv[1][0] * kv[1][1]):
         fe, wr = pmc.get(k, {}).get("FETCH_SIZE"), pmc.get(k, {}).get("WRITE_SIZE")
         tb = int((2 * fe + wr) * 1024) if fe is not None and wr is not None else None
         gbs = f"{tb / avg:.1f}" if tb else "-"
+        ins = {c: pmc.get(k, {}).get(c) for c in INSTS}
+        fmt = lambda v: f"{v:.0f}" if v is not None else "-"  # noqa: E731
         lines.append(f"| {k} | {calls} | {avg / 1e3:.1f} | {fe if fe is not None else '-'} | "
-                     f"{wr if wr is not None else '-'} | {tb if tb else '-'} | {gbs} |")
+                     f"{wr if wr is not None else '-'} | {tb if tb else '-'} | {gbs} | {fmt(ins['SQ_INSTS_VALU'])} | "
+                     f"{fmt(ins['SQ_INSTS_SALU'])} | {fmt(ins['SQ_INSTS_LDS'])} | {fmt(ins['SQ_WAVE_CYCLES'])} |")
         if tb and k.startswith(("hs_", "kt_", "gm_", "pl_")):
-            entries.append({"kernel": k, **wkey, "avg_ns": avg,
-                            "fetch_kb": fe, "write_kb": wr, "traffic_bytes_per_launch": tb,
-                            "source": f"profiles/{rnd}/{tag}_summary.md"})
+            e = {"kernel": k, **wkey, "avg_ns": avg,
+                 "fetch_kb": fe, "write_kb": wr, "traffic_bytes_per_launch": tb,
+                 "source": f"profiles/{rnd}/{tag}_summary.md"}
+            if ins["SQ_INSTS_VALU"] is not None:
+                e.update({"insts_valu": ins["SQ_INSTS_VALU"], "insts_salu": ins["SQ_INSTS_SALU"],
+                          "insts_lds": ins["SQ_INSTS_LDS"], "wave_cycles": ins["SQ_WAVE_CYCLES"],
+                          "busy_cycles": ins["SQ_BUSY_CYCLES"], "waves": ins["SQ_WAVES"]})
+            entries.append(e)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
 
@@ -84,7 +102,8 @@ def main():
     except (OSError, ValueError):
         d = {"entries": []}
     def ident(e):
-        return (e["kernel"], e["config"], e["streams"], e.get("semantics"), e.get("order"), e.get("kernel_src"))
+        return (e["kernel"], e["config"], e["streams"], e.get("semantics"), e.get("order"), e.get("kernel_src"),
+                e.get("issue_split"))
     keep = [e for e in d["entries"] if ident(e) not in {ident(n) for n in entries}]
     d["entries"] = keep + entries
     with open(path, "w") as f:

@@ -86,6 +86,9 @@ struct hs_ctx {
     // least 2 when the pipelined run (SLAM2D_PIPELINE=1) drives the two fleet halves as parts 0 and 1
     int nq = 1;
     int update_single = 1;  // hs_update_kernel (per stream-level, default) or bin + tile kernels
+    // the single-kernel update: hs_update_ring_kernel (ring-ordered tiles, ray cursors; default) or the
+    // round-3 hs_update_kernel (per-tile clipping; SLAM2D_UPD_KERNEL=clip, and scans of > 1280 points)
+    bool upd_ring = true;
     int ncu = 256;
     bool upd_parts_fixed = false;  // SLAM2D_UPD_PARTS given: no batch-size adaptive split
     // per part (a batch split over part streams): two alternating lists of updating streams
@@ -266,6 +269,14 @@ bool upd_single_ok(const hs_ctx *c)
     return c->update_single && upd_shmem_bytes(c) <= 65536 && c->sx <= 16385 && c->sy <= 16385;
 }
 
+// hs_update_ring_kernel: rays in registers (<= RING_GROUPS * 256 points), da / db in 14 bits (<= 16384
+// cells per side)
+bool upd_ring_ok(const hs_ctx *c)
+{
+    return c->upd_ring && upd_rays_in_regs(c) && c->max_points <= RING_GROUPS * UPD_THREADS && c->sx <= 16384 &&
+           c->sy <= 16384;
+}
+
 int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int xy_stride, const int *n,
                 const float2 *origo, const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s,
                 hipEvent_t wait_before_update = nullptr, const MatchIngest *mi = nullptr)
@@ -308,7 +319,11 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         UpdList *wl_next = c->wl[part][c->wl_parity[part] ^ 1];
         c->wl_parity[part] ^= 1;
         begin_timed(c, 2, s);
-        if (upd_rays_in_regs(c))
+        if (upd_ring_ok(c))
+            hipLaunchKernelGGL(hs_update_ring_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
+                               c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, wl_cur,
+                               wl_next, c->ncu);
+        else if (upd_rays_in_regs(c))
             hipLaunchKernelGGL((hs_update_kernel<UPD_RREG>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
                                c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, wl_cur,
                                wl_next, c->ncu);
@@ -339,7 +354,11 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         begin_timed(c, 2, s);
         int blocks = 0;
         for (int l = 0; l < c->levels; ++l) blocks += gg.upd_parts[l] * count;
-        if (upd_rays_in_regs(c))
+        if (upd_ring_ok(c))
+            hipLaunchKernelGGL(hs_update_ring_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
+                               c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, (const UpdList *)nullptr,
+                               (UpdList *)nullptr, c->ncu);
+        else if (upd_rays_in_regs(c))
             hipLaunchKernelGGL((hs_update_kernel<UPD_RREG>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
                                c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, (const UpdList *)nullptr,
                                (UpdList *)nullptr, c->ncu);
@@ -537,6 +556,8 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         c->nparts = np ? atoi(np) : 1;
         const char *um = getenv("SLAM2D_UPDATE");
         c->update_single = (um && strcmp(um, "binned") == 0) ? 0 : 1;  // measured: single 1.06 ms vs binned 1.30 ms
+        const char *uk = getenv("SLAM2D_UPD_KERNEL");
+        c->upd_ring = !(uk && strcmp(uk, "clip") == 0);
         // workgroups per (stream, level) of hs_update_kernel: adaptive (launch_part: 1 at >= 512 streams,
         // where splitting measured neutral to slower), or fixed by SLAM2D_UPD_PARTS="p0,p1,..." 
         for (int l = 0; l < MAX_LEVELS; ++l) c->geom.upd_parts[l] = 1;

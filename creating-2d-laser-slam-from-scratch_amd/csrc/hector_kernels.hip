@@ -2041,6 +2041,455 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     clk_stamp(geom.clk, 1, false);
 }
 
+// ------------------------------------ k2 (default, round 4): ring-ordered grid update with ray cursors
+// The same once-per-scan update as hs_update_kernel (tiles of 64 x UPD_TH cells, LDS event words + hit
+// bits, the two-stage raster / apply pipeline, fan groups culled per tile with one ballot), with the
+// per-(tile, ray) clip replaced by a cursor per ray.
+//
+// Tile order.  The tiles of the level's box are visited in RINGS around the tile of the scan's begin
+// cell: ring k = the tiles at Chebyshev distance k (in tile units), and inside a ring by the secondary
+// distance s = min(|dx|, |dy|).  Along a ray both tile coordinates move monotonically away from the
+// begin tile (the ray starts inside it), so each tile change strictly increases (k, s) in lexicographic
+// order: every ray meets its tiles in the visit order, one after the other.  So each lane keeps, per ray,
+// the walk's position -- the next step i and the minor steps q before it -- and a tile visit starts where
+// the previous one stopped: no clipping of the ray against the tile (round 3: ray_walk + walk_range + the
+// start division, ~150 VALU per (tile, fan group) visit), only the exit of the tile (one division by db
+// for the minor boundary, one by da for the minor steps taken).
+// Parts: part p of a level takes a contiguous range of rings (split by tile count, ring_split); its
+// cursors start at the first step of each ray inside its first ring (ray_cursor).
+// Per ray two registers (scans of <= RING_GROUPS * 256 points; larger scans use hs_update_kernel<0>):
+//   consts  = da | db << 14 | (x step < 0) << 28 | (y step < 0) << 29 | x major << 30   (0: no ray)
+//   cursor  = i | q << 16: step i is next, q = its minor steps (i > da: the ray is done)
+// (da, db < 2^14: maps of at most 16384 cells per side, upd_ring_ok).
+constexpr int RING_GROUPS = 5;
+constexpr unsigned CUR_DONE = 0xFFFFu;
+
+__device__ __forceinline__ unsigned ray_consts(int x0, int y0, unsigned r)
+{
+    if (r == RAY_INVALID) return 0u;
+    const int dx = (int)(r & 0xFFFFu) - x0, dy = (int)(r >> 16) - y0;
+    const int adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+    const bool xm = adx >= ady;                                   // (:252)
+    const unsigned da = (unsigned)(xm ? adx : ady), db = (unsigned)(xm ? ady : adx);
+    // util::sign (UtilFunctions.h:55-58): sign(0) = -1
+    return da | (db << 14) | ((unsigned)(dx <= 0) << 28) | ((unsigned)(dy <= 0) << 29) | ((unsigned)xm << 30);
+}
+
+// tiles of the box [tx0, tx1] x [ty0, ty1] within Chebyshev distance k of (ox, oy) (k < 0: none)
+__device__ __forceinline__ int tiles_within(int k, int ox, int oy, int tx0, int tx1, int ty0, int ty1)
+{
+    if (k < 0) return 0;
+    const int w = min(tx1, ox + k) - max(tx0, ox - k) + 1, h = min(ty1, oy + k) - max(ty0, oy - k) + 1;
+    return (w > 0 && h > 0) ? w * h : 0;
+}
+
+// The cursor of a ray at its first step inside ring >= K (K = 0: step 0).  Along x the ring starts
+// Dx cells from the begin cell (the ray's x moves away from the begin tile), along y Dy; a major-axis
+// distance D is reached at step D, a minor-axis one at the first i with q(i) = floor((e0 + i db) / da) >= D.
+__device__ __forceinline__ unsigned ray_cursor(unsigned C, int K, int x0, int y0, int ox, int oy)
+{
+    const int da = (int)(C & 0x3FFFu), db = (int)((C >> 14) & 0x3FFFu);
+    if (da == 0) return CUR_DONE;
+    if (K == 0) return 0u;
+    const bool sxn = (C >> 28) & 1u, syn = (C >> 29) & 1u, xm = (C >> 30) & 1u;
+    const int e0 = da >> 1;
+    const int Dx = sxn ? x0 - ((ox - K) * TILE + TILE - 1) : (ox + K) * TILE - x0;
+    const int Dy = syn ? y0 - ((oy - K) * UPD_TH + UPD_TH - 1) : (oy + K) * UPD_TH - y0;
+    const int INF = 0x7FFF;
+    const int Dma = xm ? Dx : Dy, Dmi = xm ? Dy : Dx;
+    const int im = Dma <= da ? Dma : INF;
+    const int in = (Dmi <= db) ? (Dmi * da - e0 + db - 1) / db : INF;  // db >= Dmi >= 1 here
+    const int i = min(im, in);
+    if (i > da) return CUR_DONE;
+    const int q = (e0 + i * db) / da;
+    return (unsigned)i | ((unsigned)q << 16);
+}
+
+// One fan group's visit of the tile at (X0, Y0) for this lane's ray (consts C, cursor S): if the cursor
+// is inside the tile, the ray's steps from there to where it leaves the tile (or ends) are marked --
+// free steps with event 2b + 1 (bresenhamCellFree, OccGridMapBase.h:302-312), the end cell with 2b and
+// its hit bit (bresenhamCellOcc, :314-330) -- and the cursor moves past them.  Direction handling is
+// select-free where it can be: with the sign masks mx, my (0 or -1), a signed step is (t ^ m) - m and
+// the steps left to a tile edge are l ^ 63 or l ^ 31 (63 - l, 31 - l for l in range) or l itself.
+__device__ __forceinline__ void ring_visit(unsigned C, unsigned &S, unsigned b, int rx0, int ry0, unsigned *marks,
+                                           unsigned *hitb, unsigned &anyv, int bm)
+{
+    const int i = (int)(S & 0xFFFFu);
+    const int q = (int)(S >> 16);
+    const int da = (int)(C & 0x3FFFu);
+    const int db = (int)((C >> 14) & 0x3FFFu);
+    const int mx = ((int)(C << 3)) >> 31, my = ((int)(C << 2)) >> 31;  // bits 28 / 29: x / y step < 0
+    const bool xm = (C >> 30) & 1u;
+    // the cursor's cell relative to the tile (rx0 = begin x - X0, ry0 = begin y - Y0)
+    const int ix = xm ? i : q, iy = xm ? q : i;
+    const int lx = rx0 + ((ix ^ mx) - mx), ly = ry0 + ((iy ^ my) - my);
+    // done rays (i > da) and cursors outside the tile: nothing here (one branch)
+    if ((int)(i > da) | (int)((unsigned)lx >= (unsigned)TILE) | (int)((unsigned)ly >= (unsigned)UPD_TH)) return;
+    // steps after this one that stay inside the tile along x / y
+    const int rx = lx ^ ((TILE - 1) & ~mx), ry = ly ^ ((UPD_TH - 1) & ~my);
+    const int ra = xm ? rx : ry, rb = xm ? ry : rx;
+    const int e = (da >> 1) + (int)__umul24((unsigned)i, (unsigned)db) - (int)__umul24((unsigned)q, (unsigned)da);
+    // steps inside the tile, this one included: the major axis leaves after ra + 1, the walk ends at step
+    // da, the minor axis leaves at the first step with rb + 1 minor steps: ceil(((rb + 1) da - e) / db)
+    int n = min(ra + 1, da - i + 1);
+    const unsigned dbs = db ? (unsigned)db : 1u;
+    const unsigned nb = udiv_rcp(__umul24((unsigned)(rb + 1), (unsigned)da) - (unsigned)e + dbs - 1u, dbs,
+                                 __builtin_amdgcn_rcpf((float)dbs));
+    n = db ? min(n, (int)nb) : n;
+    // the last step in the tile: its minor steps k after this one and its error el
+    unsigned el;
+    const int k = (int)udiv_small((unsigned)e + __umul24((unsigned)(n - 1), (unsigned)db), (unsigned)da, el);
+    const int last = i + n - 1;
+    const bool hit = last == da;
+    anyv = 1u;
+    // the cursor's next step: error el + db, a minor step iff it reaches da (a done ray keeps i = da + 1)
+    S = (unsigned)(last + 1) | ((unsigned)(q + k + (int)(el + (unsigned)db >= (unsigned)da)) << 16);
+    if (hit) {  // bresenhamCellOcc (:266): the end cell, n - 1 major and k minor steps from the cursor
+        const int ta = xm ? n - 1 : k, tb = xm ? k : n - 1;
+        const int lxl = lx + ((ta ^ mx) - mx), lyl = ly + ((tb ^ my) - my);
+        const int c = lyl * TILE + lxl;
+        atomicMin(&marks[lds_row(lyl) + lxl], 2u * b);
+        atomicOr(&hitb[c >> 5], 1u << (c & 31));
+    }
+    const int nfree = n - (int)hit;
+    if (nfree <= 0) return;
+    // start of the walk: forward lanes (bm = 0) at the cursor; backward lanes (bm = -1) at the last free
+    // step -- the last step, or the one before it when the last is the end cell (un-stepped: the end cell was
+    // reached by a minor step iff el < db)
+    const bool um = hit && el < (unsigned)db;
+    const int ts = bm & (n - 1 - (int)hit);                       // major steps from the cursor
+    const int ks = bm & (k - (int)um);                            // minor steps from the cursor
+    const int es = bm ? (int)el - (hit ? db : 0) + (um ? da : 0) : da - 1 - e;  // g = error (bwd) / f (fwd)
+    const int sxs = xm ? ts : ks, sys = xm ? ks : ts;
+    const int lxs = lx + ((sxs ^ mx) - mx), lys = ly + ((sys ^ my) - my);
+    // LDS byte steps along the major / minor axis, negated for backward lanes
+    const int dx4 = (4 ^ mx) - mx, dy4 = ((4 * UPD_STRIDE) ^ my) - my;
+    const int dab1 = xm ? dx4 : dy4, dab21 = dx4 + dy4;
+    const int dab = (dab1 ^ bm) - bm, dab2 = (dab21 ^ bm) - bm;
+    const unsigned vdn = (unsigned)db << 18;
+    const unsigned vk_major = (unsigned)dab;
+    const unsigned vk_minor = ((unsigned)da << 18) + (unsigned)dab2;
+    unsigned v = ((unsigned)es << 18) + lds_addr(marks) + (unsigned)(lds_row(lys) + lxs) * 4u;
+    const unsigned ev = 2u * b + 1u;
+    int kk = 0;
+#define S2D_WSTEP                                                          \
+    do {                                                                   \
+        upd_mark(lds_ptr(v & 0x3FFFFu), ev); /* bresenhamCellFree */       \
+        unsigned vn_;                                                      \
+        const bool c_ = __builtin_sub_overflow(v, vdn, &vn_);              \
+        v = vn_ + (c_ ? vk_minor : vk_major);                              \
+    } while (0)
+    for (; kk + 7 < nfree; kk += 8) {
+        S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
+    }
+    if (kk + 3 < nfree) {
+        S2D_WSTEP; S2D_WSTEP; S2D_WSTEP; S2D_WSTEP;
+        kk += 4;
+    }
+    if (kk + 1 < nfree) {
+        S2D_WSTEP; S2D_WSTEP;
+        kk += 2;
+    }
+#undef S2D_WSTEP
+    if (kk < nfree) upd_mark(lds_ptr(v & 0x3FFFFu), ev);
+}
+
+// The ring range [kb, ke) of part p of `parts` for a box of `total` tiles: parts split the tiles of the
+// box in ring order by count (every part's range is whole rings).
+__device__ __forceinline__ void ring_split(int p, int parts, int kmax, int ox, int oy, int tx0, int tx1, int ty0,
+                                           int ty1, int &kb, int &ke)
+{
+    kb = 0;
+    ke = kmax + 1;
+    if (parts <= 1) return;
+    const int total = tiles_within(kmax, ox, oy, tx0, tx1, ty0, ty1);
+    const int lo = (int)(((long long)total * p) / parts), hi = (int)(((long long)total * (p + 1)) / parts);
+    // kb: the first ring whose preceding rings hold >= lo tiles (p = 0: ring 0); ke likewise for hi
+    kb = p == 0 ? 0 : kmax + 1;
+    ke = p == parts - 1 ? kmax + 1 : kmax + 1;
+    for (int k = 0; k <= kmax; ++k) {
+        const int before = tiles_within(k - 1, ox, oy, tx0, tx1, ty0, ty1);
+        if (p > 0 && kb > kmax && before >= lo && k > 0) kb = k;
+        if (p < parts - 1 && ke > kmax && before >= hi && k > 0) ke = k;
+    }
+    if (ke < kb) ke = kb;
+}
+
+// Next tile of the box in ring order: candidates (k, s, j), j = 0..7 the 8 tiles (+-k, +-s), (+-s, +-k),
+// duplicates skipped (s == 0: odd j; s == k: j >= 4; k == 0: j = 0 only).  The caller knows how many
+// tiles remain, so a candidate is always found.
+struct RingIter {
+    int k, s, j;
+    int ox, oy, tx0, tx1, ty0, ty1;
+    __device__ __forceinline__ void next(int &tx, int &ty)
+    {
+        for (;;) {
+            if (++j == 8) {
+                j = 0;
+                if (++s > k) {
+                    s = 0;
+                    ++k;
+                }
+            }
+            if (k == 0 && j != 0) continue;
+            if ((s == 0 && (j & 1)) || (s == k && j >= 4)) continue;
+            const int u = j < 4 ? k : s, v = j < 4 ? s : k;
+            const int dx = ((j < 4 ? (j & 2) : (j & 1)) != 0) ? -u : u;
+            const int dy = ((j < 4 ? (j & 1) : (j & 2)) != 0) ? -v : v;
+            tx = ox + dx;
+            ty = oy + dy;
+            if (tx >= tx0 && tx <= tx1 && ty >= ty0 && ty <= ty1) return;
+        }
+    }
+};
+
+__global__ void __launch_bounds__(UPD_THREADS, S2D_UPD_MINB)
+hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restrict__ state,
+                      const float2 *__restrict__ xy, int xy_stride, const float2 *__restrict__ mc, int mc_stride,
+                      int stream_begin, int count, int max_points, const UpdList *__restrict__ wl,
+                      UpdList *__restrict__ wl_next, int ncu)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned smem[];
+    __shared__ unsigned s_any[2];
+    __shared__ unsigned s_touched;
+    int4 *gbox = reinterpret_cast<int4 *>(smem + UPD_FIXED_WORDS);  // per fan group: x0 y0 x1 y1
+    const int lane = threadIdx.x & 63;
+    __shared__ int s_bbox[4];
+
+    int lvl = 0, idx = (int)blockIdx.x, parts, part, local;
+    if (wl) {
+        const int U = wl->count;
+        if (blockIdx.x == 0 && threadIdx.x == 0) wl_next->count = 0;
+        int pl[MAX_LEVELS];
+        upd_split(U, ncu, geom.levels, pl, geom.upd_minp);
+        while (lvl + 1 < geom.levels && idx >= pl[lvl] * U) idx -= pl[lvl++] * U;
+        if (idx >= pl[lvl] * U) return;
+        parts = pl[lvl];
+        part = idx / U;
+        local = wl->stream[idx - part * U];
+    } else {
+        while (lvl + 1 < geom.levels && idx >= geom.upd_parts[lvl] * count) idx -= geom.upd_parts[lvl++] * count;
+        parts = geom.upd_parts[lvl];
+        part = idx / count;
+        local = idx - part * count;
+    }
+    const int s = stream_begin + local;
+    const StreamState &st = state[s];
+    if (!st.do_update) return;
+    clk_stamp(geom.clk, 1, true);
+    const LevelGeom &g = geom.lv[lvl];
+    const int n = lvl == 0 ? st.n : st.mc_n;  // MapRepMultiMap::updateByScan (MapRepMultiMap.h:181-188)
+    const int tid = threadIdx.x;
+    float *lvw = cells + (size_t)s * geom.stream_words + g.word_offset;
+
+    const RayFrame fr = ray_frame(g, st, lvl == 0 ? st.origo : st.mc_origo);
+    const int x0 = fr.bxi, y0 = fr.byi;
+    if (tid == 0) {
+        s_bbox[0] = x0; s_bbox[1] = y0; s_bbox[2] = x0; s_bbox[3] = y0;
+    }
+    __syncthreads();
+    int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
+    unsigned long long L = 0, R = 0;
+    const float2 *pts = lvl == 0 ? xy + (size_t)local * xy_stride : mc + (size_t)s * mc_stride;
+    const int wave_beam0 = __builtin_amdgcn_readfirstlane(tid & ~63);
+    const int wave = wave_beam0 >> 6;
+    unsigned Ck[RING_GROUPS], Sk[RING_GROUPS];
+#pragma unroll
+    for (int k = 0; k < RING_GROUPS; ++k) {
+        Ck[k] = 0u;
+        const int b0 = wave_beam0 + k * UPD_THREADS;
+        if ((b0 & ~255) >= n) continue;  // uniform: every group of a started 256-beam block gets its box
+        const int b = fan_beam(b0, lane);
+        const unsigned r = b < n ? make_ray(g, fr, pts[b]) : RAY_INVALID;
+        Ck[k] = ray_consts(x0, y0, r);
+        int gx0 = x0, gy0 = y0, gx1 = x0, gy1 = y0;  // fan group box: origin + valid ends
+        if (r != RAY_INVALID) {
+            const int x1 = (int)(r & 0xFFFFu), y1 = (int)(r >> 16);
+            gx0 = min(gx0, x1); gy0 = min(gy0, y1); gx1 = max(gx1, x1); gy1 = max(gy1, y1);
+            L += (unsigned long long)((Ck[k] & 0x3FFFu) + 1u);
+            R += 1;
+        }
+        bx0 = min(bx0, gx0); by0 = min(by0, gy0); bx1 = max(bx1, gx1); by1 = max(by1, gy1);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            gx0 = min(gx0, __shfl_xor(gx0, off, 64));
+            gy0 = min(gy0, __shfl_xor(gy0, off, 64));
+            gx1 = max(gx1, __shfl_xor(gx1, off, 64));
+            gy1 = max(gy1, __shfl_xor(gy1, off, 64));
+        }
+        if (lane == 0) gbox[b0 >> 6] = make_int4(gx0, gy0, gx1, gy1);
+    }
+    if (R) {
+        atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
+        atomicMax(&s_bbox[2], bx1); atomicMax(&s_bbox[3], by1);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        L += __shfl_xor(L, off, 64);
+        R += __shfl_xor(R, off, 64);
+    }
+    if (lane == 0 && R && part == 0) {
+        atomicAdd(&state[s].step_cells, L);
+        atomicAdd(&state[s].tot_cells, L);
+        atomicAdd(&state[s].tot_rays, R);
+    }
+    for (int k = tid; k < 2 * UPD_MARK_WORDS / 4; k += UPD_THREADS)
+        reinterpret_cast<uint4 *>(smem)[k] = (k % (UPD_MARK_WORDS / 4)) < UPD_TILE_WORDS / 4
+                                                 ? make_uint4(W_NONE, W_NONE, W_NONE, W_NONE)
+                                                 : make_uint4(0u, 0u, 0u, 0u);
+    if (tid < 2) s_any[tid] = 0u;
+    if (tid == 0) s_touched = 0u;
+    if (!__syncthreads_or(R != 0)) {  // no ray drawn on this level
+        clk_stamp(geom.clk, 1, false);
+        return;
+    }
+    const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / UPD_TH;
+    const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / UPD_TH;
+    const int ox = x0 / TILE, oy = y0 / UPD_TH;  // the begin tile (x0, y0 >= 0: valid rays start inside the map)
+    const int kmax = max(max(ox - tx0, tx1 - ox), max(oy - ty0, ty1 - oy));
+    int kb, ke;
+    ring_split(part, parts, kmax, ox, oy, tx0, tx1, ty0, ty1, kb, ke);
+    const int my_tiles = tiles_within(ke - 1, ox, oy, tx0, tx1, ty0, ty1) - tiles_within(kb - 1, ox, oy, tx0, tx1, ty0, ty1);
+#pragma unroll
+    for (int k = 0; k < RING_GROUPS; ++k) Sk[k] = ray_cursor(Ck[k], kb, x0, y0, ox, oy);
+    const int mark_free = st.mark_base + 1;  // currMarkFreeIndex (:120)
+    const int mark_occ = st.mark_base + 2;   // currMarkOccIndex  (:121)
+    const float lf = geom.lf, lo = geom.lo;
+    unsigned touched = 0;
+    const int nfans = ((n + UPD_THREADS - 1) / UPD_THREADS) * (UPD_THREADS / 64);
+    const int bm = -(lane & 1);  // odd lanes (bm = -1) walk their segments backwards (see hs_update_kernel)
+    RingIter it;
+    it.k = kb;
+    it.s = 0;
+    it.j = -1;
+    it.ox = ox; it.oy = oy; it.tx0 = tx0; it.tx1 = tx1; it.ty0 = ty0; it.ty1 = ty1;
+
+    float4 ql[UPD_QUADS];
+    unsigned qb[UPD_QUADS];
+    float *pend_tl = nullptr;
+    for (int ii = 0; ii <= my_tiles; ++ii) {
+        const int i = __builtin_amdgcn_readfirstlane(ii);
+        const int buf = i & 1;
+        unsigned *marks = smem + buf * UPD_MARK_WORDS;
+        unsigned *hitb = marks + UPD_TILE_WORDS;
+        int tx = 0, ty = 0;
+        if (i < my_tiles) {
+            it.next(tx, ty);
+            const int X0 = tx * TILE, Y0 = ty * UPD_TH;
+            const int X1 = X0 + TILE, Y1 = Y0 + UPD_TH;
+            unsigned anyv = 0u;
+            unsigned long long fm;
+            {
+                int ol = lane;
+                asm volatile("" : "+v"(ol));
+                const int4 gb = gbox[min(ol, nfans - 1)];
+                fm = __ballot((int)(ol < nfans) & (int)(gb.z >= X0) & (int)(gb.x < X1) & (int)(gb.w >= Y0) &
+                              (int)(gb.y < Y1));
+            }
+            const int rx0 = x0 - X0, ry0 = y0 - Y0;
+            // this wave's groups (fi = wave + 4 k) that meet the tile, one set bit each (scalar find-first-set);
+            // the visit exists once, its group's two registers picked and written back by scalar branches
+            unsigned long long gm = fm & (0x1111111111111111ull << wave);
+            while (gm) {
+                const int k = __builtin_ctzll(gm) >> 2;
+                gm &= gm - 1ull;
+                unsigned C, S;
+                switch (k) {
+                case 0: C = Ck[0]; S = Sk[0]; break;
+                case 1: C = Ck[1]; S = Sk[1]; break;
+                case 2: C = Ck[2]; S = Sk[2]; break;
+                case 3: C = Ck[3]; S = Sk[3]; break;
+                default: C = Ck[4]; S = Sk[4]; break;
+                }
+                const unsigned b = (unsigned)fan_beam(wave_beam0 + k * UPD_THREADS, lane);
+                ring_visit(C, S, b, rx0, ry0, marks, hitb, anyv, bm);
+                switch (k) {
+                case 0: Sk[0] = S; break;
+                case 1: Sk[1] = S; break;
+                case 2: Sk[2] = S; break;
+                case 3: Sk[3] = S; break;
+                default: Sk[4] = S; break;
+                }
+            }
+            if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see hs_update_kernel
+        if (pend_tl) {
+            int *tu = reinterpret_cast<int *>(pend_tl + TILE_CELLS);
+            // the quads' offsets are recomputed per tile from an opaque copy of tid (a few VALU): hoisted out of
+            // the tile loop they were held in registers the cursors need, and spilled
+            int tq = tid;
+            asm volatile("" : "+v"(tq));
+#pragma unroll
+            for (int j = 0; j < UPD_QUADS; ++j) {
+                const unsigned mb = qb[j];
+                if (!(mb & 15u)) continue;
+                const int qi = tq + j * UPD_THREADS;
+                const unsigned o = (unsigned)upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
+                float4 v = ql[j];
+                const float lv[4] = {v.x, v.y, v.z, v.w};
+                float nv[4];
+                int uv[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float l = lv[c];
+                    const float t = l + lf;                       // updateSetFree
+                    const float u = t - lf;                       // ... then updateUnsetFree
+                    const float h = bit_select(mb, 4 + c, u, l);  // an earlier beam freed the hit cell
+                    const float oc = h < 50.0f ? h + lo : h;      // updateSetOccupied
+                    nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);
+                    uv[c] = __float_as_int(bit_select(mb, 8 + c, __int_as_float(mark_occ), __int_as_float(mark_free)));
+                }
+                *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);
+                if ((mb & 15u) == 15u) {
+                    *reinterpret_cast<int4 *>(&tu[o]) = make_int4(uv[0], uv[1], uv[2], uv[3]);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        if ((mb >> c) & 1u) tu[o + (unsigned)c] = uv[c];
+                }
+                touched += __popc(mb & 15u);
+            }
+            pend_tl = nullptr;
+        }
+        if (i < my_tiles) {
+            lds_barrier();  // tile i's marks complete
+            if (s_any[buf] == (unsigned)(i + 1)) {
+                pend_tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
+                int tq = tid;
+                asm volatile("" : "+v"(tq));
+#pragma unroll
+                for (int j = 0; j < UPD_QUADS; ++j) {
+                    const unsigned qi = (unsigned)tq + j * UPD_THREADS;
+                    const int row = (int)(qi >> 4), c4 = (int)((qi & 15u) << 2);
+                    const int mw = lds_row(row) + c4;
+                    const uint4 m = *reinterpret_cast<const uint4 *>(&marks[mw]);
+                    const unsigned h = (hitb[row * (TILE / 32) + (c4 >> 5)] >> (c4 & 31)) & 15u;
+                    const unsigned mk = (unsigned)(m.x != W_NONE) | ((unsigned)(m.y != W_NONE) << 1) |
+                                        ((unsigned)(m.z != W_NONE) << 2) | ((unsigned)(m.w != W_NONE) << 3);
+                    const unsigned od = (m.x & 1u) | ((m.y & 1u) << 1) | ((m.z & 1u) << 2) | ((m.w & 1u) << 3);
+                    qb[j] = mk | ((od & mk) << 4) | ((h & mk) << 8);
+                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));
+                    if (mk) {
+                        // "no mark" from an opaque register: a hoisted all-ones quad was held across the loop
+                        // and spilled (its reload waited for the quad loads just issued)
+                        unsigned none = W_NONE;
+                        asm volatile("" : "+v"(none));
+                        *reinterpret_cast<uint4 *>(&marks[mw]) = make_uint4(none, none, none, none);
+                    }
+                    if ((tid & 7) == 0) hitb[row * (TILE / 32) + (c4 >> 5)] = 0u;
+                }
+            }
+        }
+    }
+    // distinct cells written: summed in LDS (a shuffle reduction here had its lane addresses hoisted to the
+    // kernel's start and spilled)
+    if (touched) atomicAdd(&s_touched, touched);
+    __syncthreads();
+    if (tid == 0 && s_touched) atomicAdd(&state[s].tot_touched, (unsigned long long)s_touched);
+    clk_stamp(geom.clk, 1, false);
+}
+
 // --------------------------------------------------------------------------- utility kernels
 __global__ void hs_fill_cells_kernel(float *__restrict__ words, size_t n)
 {

@@ -4,18 +4,20 @@ TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 export TMPDIR=/tmp
 cd /tmp
-for v in "$@"; do
+for spec in "$@"; do
+  v=${spec%%+*}; envs=""; [ "$spec" != "$v" ] && envs=${spec#*+}
   if [ "$v" = main ]; then lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/libslam2d.so; else lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/libslam2d_$v.so; fi
   [ -f "$lib" ] || { echo "missing $lib"; exit 1; }
-  OUT=$ROOT/gpurun_out/pmcab_${TAG}_$v; mkdir -p "$OUT"
+  tagv=$(echo "$spec" | tr '+=' '__')
+  OUT=$ROOT/gpurun_out/pmcab_${TAG}_$tagv; mkdir -p "$OUT"
   i=0
   for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
              "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" \
              "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_ADDR_CONFLICT"; do
     i=$((i+1))
-    SLAM2D_LIB=$lib timeout -k 10 120 rocprofv3 --pmc $set -d "$OUT/p$i" -o run --output-format csv -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-copy-probe --steps 5 --warmup 2 > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+    env SLAM2D_LIB=$lib $envs timeout -k 10 120 rocprofv3 --pmc $set -d "$OUT/p$i" -o run --output-format csv -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-copy-probe --steps 5 --warmup 2 > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   done
-  python3 - "$OUT" "$v" <<'PY'
+  python3 - "$OUT" "$tagv" <<'PY'
 import csv, glob, os, sys, collections
 agg = collections.defaultdict(float); cnt = collections.Counter()
 for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):

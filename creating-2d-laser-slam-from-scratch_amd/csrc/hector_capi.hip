@@ -293,14 +293,20 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     const bool use_list = single && !c->upd_parts_fixed && mode != MODE_MATCH_ONLY;
     UpdList *wl_cur = use_list ? c->wl[part][c->wl_parity[part]] : nullptr;
     begin_timed(c, 0, s);
-    if (c->reduce_order == 0)
-        hipLaunchKernelGGL(hs_match_kernel<true>, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state,
-                           xy, xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur, c->ingest,
-                           mi ? *mi : MatchIngest{}, c->d_ixy, c->max_points);
-    else
-        hipLaunchKernelGGL(hs_match_kernel<false>, dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells, c->d_state,
-                           xy, xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur, c->ingest,
-                           mi ? *mi : MatchIngest{}, c->d_ixy, c->max_points);
+    // the register-only instance when no scan of the context can exceed the kernel's register slots
+    const MatchIngest mik = mi ? *mi : MatchIngest{};
+#define S2D_MATCH_LAUNCH(SEQ, REGS)                                                                                      \
+    hipLaunchKernelGGL((hs_match_kernel<SEQ, REGS>), dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells,         \
+                       c->d_state, xy, xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur,   \
+                       c->ingest, mik, c->d_ixy, c->max_points)
+    if (c->reduce_order == 0) {
+        if (c->max_points <= (S2D_MATCH_CW ? CW_MAXN : MATCH_THREADS * MATCH_REG_PTS)) S2D_MATCH_LAUNCH(true, true);
+        else S2D_MATCH_LAUNCH(true, false);
+    } else {
+        if (c->max_points <= MATCH_THREADS * MATCH_REG_PTS) S2D_MATCH_LAUNCH(false, true);
+        else S2D_MATCH_LAUNCH(false, false);
+    }
+#undef S2D_MATCH_LAUNCH
     end_timed(c, s);
     HCHK(hipGetLastError());
     if (mode == MODE_MATCH_ONLY) return HS_OK;

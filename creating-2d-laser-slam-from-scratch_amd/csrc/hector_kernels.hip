@@ -342,9 +342,10 @@ constexpr int SEQ_WORDS = 9 * SEQ_STRIDE;
 // run + T[lane][0] + T[lane][1] + ... + T[lane][cnt - 1], left to right.  The adds are one dependent
 // chain; the LDS reads of the next 16 terms are issued before the current 16 are added.
 #define S2D_ADD4(v) do { run = run + (v).x; run = run + (v).y; run = run + (v).z; run = run + (v).w; } while (0)
-__device__ __forceinline__ float seq_chain(const float *T, int lane, int cnt, float run)
+template <int STRIDE>
+__device__ __forceinline__ float seq_chain_t(const float *T, int lane, int cnt, float run)
 {
-    const float4 *row = reinterpret_cast<const float4 *>(T + lane * SEQ_STRIDE);
+    const float4 *row = reinterpret_cast<const float4 *>(T + lane * STRIDE);
     const int c4 = cnt >> 2;
     int i = 0;
     if (c4 >= 8) {
@@ -366,11 +367,15 @@ __device__ __forceinline__ float seq_chain(const float *T, int lane, int cnt, fl
         const float4 a = row[i];
         S2D_ADD4(a);
     }
-    const float *tail = T + lane * SEQ_STRIDE + (c4 << 2);
+    const float *tail = T + lane * STRIDE + (c4 << 2);
     for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];
     return run;
 }
 #undef S2D_ADD4
+__device__ __forceinline__ float seq_chain(const float *T, int lane, int cnt, float run)
+{
+    return seq_chain_t<SEQ_STRIDE>(T, lane, cnt, run);
+}
 
 // The wave that runs a workgroup's sequential sums and step tail.  Workgroups co-resident on one CU
 // tend to have block ids 256 apart (round-robin dispatch over the CUs), so the block id's bits 8-9 are
@@ -721,6 +726,192 @@ __device__ __forceinline__ void gn_step_reg(const float *__restrict__ cells, con
     for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];
 }
 
+// ---- the reference's summation order with a dedicated chain wave (default, round 4) ---------------
+// Round 3 ran the sequential sums on one wave that ALSO computed a quarter of every chunk's terms, so each
+// chunk cost the chain (256 dependent adds) plus that wave's share of the next chunk's terms, and the
+// other waves waited for it at every hand-off (chunk loop 15.4 k of a GN step's 24 k cycles).  Here the
+// chain wave cw holds no points: the other three waves own the scan (point i = chunk * CW_PTS + pt, pt the
+// thread's rank among the 192 point threads, CW_NP slots each: scans of <= 1152 points) and fill two
+// alternating term buffers, one barrier per chunk -- at barrier j the point waves have stored chunk j and
+// the chain wave has finished chunk j - 1, whose buffer the point waves fill next.  The chain wave goes from
+// chunk to chunk without waiting for terms.  The adds are the same chain in the same order as
+// getCompleteHessianDerivs (OccGridMapUtil.h:94-126), so H / b are bit-identical to round 3's.
+constexpr int CW_PTS = MATCH_THREADS - 64;        // point threads
+constexpr int CW_NP = 6;                           // slots per point thread
+constexpr int CW_MAXN = CW_PTS * CW_NP;            // 1152 points in registers
+constexpr int CW_STRIDE = CW_PTS + 4;              // term-buffer row (words): 16-B aligned, row k on bank 4k
+constexpr int CW_BUF = 9 * CW_STRIDE;              // one chunk's terms
+// term buffers: 2 (one barrier per chunk; 38.6 KB of LDS, 4 workgroups per CU) or 1 (two barriers per chunk;
+// 31.6 KB with REGS, 5 workgroups per CU)
+#ifndef S2D_CW_BUFS
+#define S2D_CW_BUFS 2
+#endif
+constexpr int CW_BUFS = S2D_CW_BUFS;
+#ifndef S2D_MATCH_CW
+#define S2D_MATCH_CW 1  // 0: round 3's chain wave that also computes terms (A/B builds)
+#endif
+
+template <int NP>
+__device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
+                                           int n, float f, float *est, float &cs, float &sn, float *H, int parity,
+                                           unsigned *nb_key, float4 *nb_val, float (*s_pose)[POSE_WORDS], float *seqT,
+                                           int cw, int pt)
+{
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = tid >> 6;
+    const int nch = (n + CW_PTS - 1) / CW_PTS;  // chunks (uniform)
+    float run = 0.0f;                           // chain wave, lane k < 9: the running sum of term k
+    if (wave != cw) {
+        // the gathered log-odds of the moved points (the transform is recomputed for the terms below: keeping
+        // px, py, fx, fy of every slot across the chunk loop cost more registers than 4 VALU per point)
+        float lg[NP][4];
+        unsigned key[NP];
+        bool miss[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            const int slot = pt + j * CW_PTS;
+            miss[j] = false;
+            key[j] = NB_NONE;
+            if (slot < n) {
+                const float px = p[j].x * f, py = p[j].y * f;
+                const float nsn = -sn;
+                const float x = est[0] + (cs * px + nsn * py);
+                const float y = est[1] + (sn * px + cs * py);
+                if ((x >= 0.0f) && (x <= g.lim[0]) && (y >= 0.0f) && (y <= g.lim[1])) {  // NaN -> out of map
+                    const int ix = (int)x, iy = (int)y;
+                    key[j] = ((unsigned)iy << 16) | (unsigned)ix;
+                    miss[j] = nb_key[slot] != key[j];
+                    if (miss[j]) {
+                        const unsigned ux = (unsigned)ix, uy = (unsigned)iy;
+                        const float *r0 = cells + cell_word(g, (int)ux, (int)uy);
+                        const float *r1 = cells + cell_word(g, (int)ux, (int)(uy + 1));
+                        if ((ux & (CELL_BLK - 1)) != CELL_BLK - 1) {  // (ix, ix + 1) adjacent in a block row
+                            float2 a, b;
+                            __builtin_memcpy(&a, r0, 8);
+                            __builtin_memcpy(&b, r1, 8);
+                            lg[j][0] = a.x; lg[j][1] = a.y; lg[j][2] = b.x; lg[j][3] = b.y;
+                        } else {
+                            lg[j][0] = r0[0];
+                            lg[j][1] = cells[cell_word(g, (int)(ux + 1), (int)uy)];
+                            lg[j][2] = r1[0];
+                            lg[j][3] = cells[cell_word(g, (int)(ux + 1), (int)(uy + 1))];
+                        }
+                    }
+                }
+            }
+        }
+        // park the gathered log-odds of every miss in its slot and list the slot for this wave (the list lives
+        // in the last term buffer: with two, first written after chunk 0's barrier; with one, chunk 0 is stored
+        // after a barrier that follows every wave's conversions), then convert 64 at a time
+        const int pw = pt >> 6;
+        unsigned short *wl = reinterpret_cast<unsigned short *>(seqT + (CW_BUFS - 1) * CW_BUF) + pw * (NP * 64);
+        int nmiss = 0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            const int slot = pt + j * CW_PTS;
+            const unsigned long long bm = __ballot(miss[j]);
+            if (miss[j]) {
+                nb_val[slot] = make_float4(lg[j][0], lg[j][1], lg[j][2], lg[j][3]);
+                nb_key[slot] = key[j];
+                wl[nmiss + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] =
+                    (unsigned short)slot;
+            }
+            nmiss += __popcll(bm);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int e = lane; e < nmiss; e += 64) {
+            const int slot = wl[e];
+            const float4 v = nb_val[slot];
+            nb_val[slot] = make_float4(cell_prob(v.x), cell_prob(v.y), cell_prob(v.z), cell_prob(v.w));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // chunk j = slot j of every point thread, in point order; buffer j & 1
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            if (j >= nch) break;  // uniform
+            const int slot = pt + j * CW_PTS;
+            if (slot < n) {
+                float t[9];
+                PointFetch pf;  // the gather phase's transform, recomputed (the same operations, the same bits)
+                pf.px = p[j].x * f;
+                pf.py = p[j].y * f;
+                const float nsn = -sn;
+                const float x = est[0] + (cs * pf.px + nsn * pf.py);
+                const float y = est[1] + (sn * pf.px + cs * pf.py);
+                pf.in = (x >= 0.0f) && (x <= g.lim[0]) && (y >= 0.0f) && (y <= g.lim[1]);
+                if (pf.in) {
+                    pf.fx = x - (float)(int)x;
+                    pf.fy = y - (float)(int)y;
+                    const float4 v = nb_val[slot];
+                    pf.l[0] = v.x; pf.l[1] = v.y; pf.l[2] = v.z; pf.l[3] = v.w;
+                }
+                point_terms<true>(pf, cs, sn, t);
+                if (CW_BUFS == 1) lds_barrier();  // the chain wave is done with chunk j - 1 (j = 0: the miss lists)
+                float *T = seqT + (CW_BUFS == 2 ? (j & 1) * CW_BUF : 0);
+#pragma unroll
+                for (int k = 0; k < 9; ++k) T[k * CW_STRIDE + pt] = t[k];
+            } else if (CW_BUFS == 1) {
+                lds_barrier();
+            }
+            lds_barrier();  // chunk j stored (two buffers: and the chain wave is done with chunk j - 1)
+        }
+    } else {
+        // the chain: lane k < 9 extends the sum of term k over each chunk, at s_setprio 3 through the step tail
+        // (the workgroup's critical path issues ahead of co-resident workgroups' waves)
+        __builtin_amdgcn_s_setprio(3);
+        for (int j = 0; j < nch; ++j) {
+            if (CW_BUFS == 1) lds_barrier();
+            lds_barrier();
+            if (lane < 9)
+                run = seq_chain_t<CW_STRIDE>(seqT + (CW_BUFS == 2 ? (j & 1) * CW_BUF : 0), lane, min(CW_PTS, n - j * CW_PTS),
+                                             run);
+        }
+    }
+    float *sp = s_pose[parity];
+    if (wave == cw) {
+        float s[9];
+        seq_gather(run, s);
+        float b[3] = {s[0], s[1], s[2]};
+        H[0] = s[3]; H[4] = s[4]; H[8] = s[5];
+        H[1] = s[6]; H[2] = s[7]; H[5] = s[8];
+        H[3] = H[1]; H[6] = H[2]; H[7] = H[5];
+        float clamp = 0.0f;
+        if ((H[0] != 0.0f) && (H[4] != 0.0f)) {
+            float d[3];
+            solve3(H, b, d);
+            if (d[2] > 0.2f) {
+                d[2] = 0.2f;
+                clamp = 1.0f;
+            } else if (d[2] < -0.2f) {
+                d[2] = -0.2f;
+                clamp = 1.0f;
+            }
+            est[0] = est[0] + d[0];
+            est[1] = est[1] + d[1];
+            est[2] = est[2] + d[2];
+        }
+        if (lane == 0) {
+            sp[0] = est[0];
+            sp[1] = est[1];
+            sp[2] = est[2];
+            sp[3] = sdm_cosf(est[2]);
+            sp[4] = sdm_sinf(est[2]);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) sp[5 + k] = H[k];
+            sp[14] = clamp;
+        }
+        __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();
+    est[0] = sp[0];
+    est[1] = sp[1];
+    est[2] = sp[2];
+    cs = sp[3];
+    sn = sp[4];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];
+}
+
 constexpr int MATCH_REG_PTS = 5;  // points per thread kept in registers: scans of up to 1280 points
 
 // register budget knob: waves per SIMD the compiler must fit the match kernel into (1 = unconstrained)
@@ -730,7 +921,10 @@ constexpr int MATCH_REG_PTS = 5;  // points per thread kept in registers: scans 
 // SEQ (default): H / b summed in the reference's sequential point order; else the tree order
 // (SLAM2D_MATCH_ORDER=tree / hs_set_reduction_order: faster, poses within float reassociation of the
 // reference's).
-template <bool SEQ>
+// REGS: every scan of the launch fits the registers (max_points <= CW_MAXN for SEQ, 1280 for the tree
+// order): the HBM-strided Gauss-Newton path is compiled out -- it alone lifted the kernel from 83 to 140
+// VGPRs (SEQ), so the common case no longer pays its register allocation
+template <bool SEQ, bool REGS>
 __global__ void __launch_bounds__(MATCH_THREADS) __attribute__((amdgpu_waves_per_eu(S2D_MATCH_WAVES)))
 hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__restrict__ state,
                 const float2 *__restrict__ xy, int xy_stride, const int *__restrict__ counts,
@@ -740,10 +934,16 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
 {
     static_assert(MATCH_THREADS == 64 * MATCH_WAVES && MATCH_WAVES == 4, "reduction tree assumes 4 waves");
     __shared__ float red[2][MATCH_WAVES][9];
-    __shared__ __attribute__((aligned(16))) float seqT[SEQ ? SEQ_WORDS : 4];  // SEQ: one chunk's terms
-    __shared__ unsigned nb_key[MATCH_REG_PTS * MATCH_THREADS];
-    __shared__ float4 nb_val[MATCH_REG_PTS * MATCH_THREADS];
-    __shared__ unsigned short mlist[MATCH_REG_PTS * MATCH_THREADS];  // per wave: slots whose cell moved
+    // SEQ: two chunks' terms for the chain wave (gn_step_cw; its miss lists live in the second), or one
+    // 256-point chunk of the HBM path (gn_step); tree order: the miss lists
+    constexpr bool CW = SEQ && S2D_MATCH_CW;                          // gn_step_cw (else round 3's gn_step_reg)
+    constexpr int NPR = CW ? CW_NP : MATCH_REG_PTS;                   // point slots per thread in registers
+    constexpr int NSLOT = CW ? CW_MAXN : MATCH_REG_PTS * MATCH_THREADS;
+    constexpr int SEQ_LDS = !CW ? SEQ_WORDS : ((CW_BUFS * CW_BUF > SEQ_WORDS || REGS) ? CW_BUFS * CW_BUF : SEQ_WORDS);
+    __shared__ __attribute__((aligned(16))) float seqT[SEQ ? SEQ_LDS : 4];
+    __shared__ unsigned nb_key[NSLOT];
+    __shared__ float4 nb_val[NSLOT];
+    __shared__ unsigned short mlist[CW ? 4 : MATCH_REG_PTS * MATCH_THREADS];  // tree order: per wave, the slots whose cell moved
     __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity
     const int local = blockIdx.x;
     const int s = stream_begin + local;
@@ -782,13 +982,19 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     if (mode == MODE_PROCESS || mode == MODE_MATCH_ONLY) {
         // MapRepMultiMap::matchData  H/slam_main/MapRepMultiMap.h:144-167
         float tmp[3] = {hint[0], hint[1], hint[2]};
-        const bool in_regs = n <= MATCH_THREADS * MATCH_REG_PTS;
-        float2 preg[MATCH_REG_PTS];
+        // SEQ: the chain wave cw holds no points; point thread pt owns points pt + j * CW_PTS (gn_step_cw)
+        const int cw = chain_wave();
+        const int wv = (int)threadIdx.x >> 6;
+        const bool owner = !CW || wv != cw;
+        const int pt = CW ? ((wv < cw ? wv : wv - 1) * 64 + ((int)threadIdx.x & 63)) : (int)threadIdx.x;
+        const int pstride = CW ? CW_PTS : MATCH_THREADS;
+        const bool in_regs = n <= pstride * NPR;
+        float2 preg[NPR];
 #pragma unroll
-        for (int j = 0; j < MATCH_REG_PTS; ++j) {
-            const int i = threadIdx.x + j * MATCH_THREADS;
+        for (int j = 0; j < NPR; ++j) {
+            const int i = pt + j * pstride;
             preg[j] = make_float2(0.0f, 0.0f);
-            if (in_regs && i < n) {
+            if (owner && in_regs && i < n) {
                 if (fused) preg[j] = stage[i];  // LDS (kept apart from the global read: no flat access)
                 else preg[j] = pts[i];
             }
@@ -802,9 +1008,9 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
         if (mcs && mcs != pts && geom.levels > 1) {
             if (in_regs) {
 #pragma unroll
-                for (int j = 0; j < MATCH_REG_PTS; ++j) {
-                    const int i = threadIdx.x + j * MATCH_THREADS;
-                    if (i < n) mcs[i] = preg[j];
+                for (int j = 0; j < NPR; ++j) {
+                    const int i = pt + j * pstride;
+                    if (owner && i < n) mcs[i] = preg[j];
                 }
             } else {
                 for (int i = threadIdx.x; i < n; i += MATCH_THREADS) mcs[i] = pts[i];
@@ -818,14 +1024,19 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             float est[3], H[9];
             map_from_world(g, tmp, est);
 #pragma unroll
-            for (int j = 0; j < MATCH_REG_PTS; ++j) nb_key[threadIdx.x + j * MATCH_THREADS] = NB_NONE;  // own slots
+            for (int j = 0; j < NPR; ++j)
+                if (owner) nb_key[pt + j * pstride] = NB_NONE;  // own slots
             float cs = sdm_cosf(est[2]), sn = sdm_sinf(est[2]);
             for (int it = 0; it <= iters; ++it) {
                 if (in_regs) {
-                    gn_step_reg<MATCH_REG_PTS, SEQ>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, red, parity, nb_key,
-                                                    nb_val, mlist, s_pose, seqT);
+                    if constexpr (CW)
+                        gn_step_cw<NPR>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, parity, nb_key, nb_val, s_pose, seqT,
+                                        cw, pt);
+                    else
+                        gn_step_reg<NPR, SEQ>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, red, parity, nb_key,
+                                              nb_val, mlist, s_pose, seqT);
                     clamps += s_pose[parity][14] != 0.0f ? 1 : 0;
-                } else {
+                } else if constexpr (!REGS) {
                     gn_step<SEQ>(lc, g, pts, n, g.pts_scale, est, H, red, parity, &clamps, seqT);
                 }
                 parity ^= 1;

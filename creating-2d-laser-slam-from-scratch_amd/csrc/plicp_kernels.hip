@@ -118,8 +118,9 @@ __device__ __forceinline__ void pl_theta_cells(double wx, double wy, int n, doub
     auto sc = [&](double th) { return (int)((th - min_theta) / (max_theta - min_theta) * n); };
     auto cc = [&](double th) { return angle_inc > 0.0 ? (int)((th - min_theta) / angle_inc) : 0; };
     const float fx = (float)wx, fy = (float)wy;
-    // zero or subnormal magnitudes (their float rounding is not relative to 2^-24) take the exact path
-    if (fx != 0.0f && fy != 0.0f && fmaxf(fabsf(fx), fabsf(fy)) >= 1.17549435e-38f) {
+    // a zero or subnormal component (its float rounding is not relative to 2^-24) takes the exact path:
+    // both magnitudes must be normal floats (the smaller one decides)
+    if (fminf(fabsf(fx), fabsf(fy)) >= 1.17549435e-38f) {
         const double a = (double)pl_fatan2(fy, fx);
         // near +-pi the exact atan2 may sit on the other side of the cut: no bracket there
         if (fabs(a) <= SDM_PI - 4.0 * PL_ATAN_EPS) {

@@ -286,3 +286,14 @@ def test_north_star_targets_block():
     assert t["read_roofline_model"]["pass"] and not t["read_roofline_counted"]["pass"]
     assert t["pose_error_m"]["pass"] and t["pose_error_rad"]["pass"]
     assert bench.north_star_targets(1.0, None, None, pose)["x_cpu_1core"]["pass"] is None
+
+
+def test_diagnostic_build_anchors_apply():
+    """tools/build_diag.py's pricing variants are textual patches of the kernel sources: every anchor must
+    still occur exactly once, so a listed variant never fails at build time on the GPU box."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("build_diag", os.path.join(bench.REPO, "tools", "build_diag.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    assert m.check() == []

@@ -6,28 +6,23 @@
 The product sources carry no wrong-result switches: every variant here is a textual patch applied to
 a temporary copy of csrc/ (the build fails loudly if a patch no longer applies).  Variants marked
 WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); never ship them.
+`python tools/build_diag.py --check` lists variants whose anchors went stale (a CPU test runs it); round 4
+removed those of the round-3 kernels it replaced (clk, dwordq, fullstore, mclk, noapply, noapplymath,
+nosetup, notiles, seq4acc: see git history before round 4).  The hs_update_kernel variants below price the
+round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
 
   plain      WRONG RESULTS  hs_update_kernel marks with plain LDS stores instead of atomicMin
-  noapply    WRONG RESULTS  hs_update_kernel skips the apply phase (no global loads / stores)
   hwexp      WRONG RESULTS  hs_match_kernel uses the hardware exp instead of (float)exp(double)
   gmplain    WRONG RESULTS  gm_compute_kernel walks with plain LDS stores instead of atomicAdd
   gmnowalk   WRONG RESULTS  gm_compute_kernel clips every line to the tile but skips the walk
   nowalk     WRONG RESULTS  hs_update_kernel clips every ray to the tile but skips the Bresenham walk
   plfastatan WRONG RESULTS  pl_icp_kernel uses float atan / atan2 (prices the exact double ones)
-  nosetup    WRONG RESULTS  hs_update_kernel keeps the fan-group culling of every tile, skips every ray (the
-                            tile loop skeleton: culling ballot, barriers, empty applies)
   ktnorender WRONG RESULTS  kt_addscans_kernel clears, loads and stores its tiles but renders no item
   lds6       same results   hs_update_kernel with 8.2 KB of unused LDS (8 -> 6 workgroups per CU: occupancy price)
   lds4       same results   hs_update_kernel with 21 KB of unused LDS (4 workgroups per CU)
   frozen     WRONG RESULTS  hs_match_kernel runs no Gauss-Newton iteration (pose = hint): the rays no longer depend
                             on the map, so an update-kernel pricing variant built as frozen__<variant> and timed
                             against frozen alone is not confounded by a drifting match
-  notiles    WRONG RESULTS  hs_update_kernel returns after building the rays and fan boxes (prices the tile loop)
-  clk        same results   hs_update_kernel accumulates per-wave clock64() cycles of its tile-loop phases into
-                            the stream counters (gn_points: raster, updates: pending apply, steps: barrier wait,
-                            touched: mark read) -- counters() then reads the phase split, tools/clk_update.py
-  noapplymath WRONG RESULTS hs_update_kernel's apply stores l + lf for every marked cell (prices the cell math)
-  fullstore  WRONG RESULTS  hs_update_kernel stores whole updateIndex quads (prices the per-cell partial stores)
   ktnoswar   WRONG RESULTS  kt_addscans_kernel dword render writes the kernel bytes without the byte max
   ktnomerge  WRONG RESULTS  kt_build_kernel skips the 64-bit CAS merge of its tile into the match grid
   ktstore    WRONG RESULTS  kt_build_kernel merges with plain stores instead of compare-and-swap
@@ -42,19 +37,11 @@ WRONG RESULTS only price a phase of a kernel (tools/ab_bench.sh times them); nev
                             32-cell half-row words (round 3), i.e. the atomicOr is not what this variant saves
   seqnochain WRONG RESULTS  hs_match_kernel's sequential sum adds one term per chunk (prices the chain adds;
                             the chunk hand-offs and barriers stay)
-  mclk       same results   hs_match_kernel accumulates the chain wave's clock64() cycles per phase of each
-                            reference-order Gauss-Newton step into the stream counters (steps: inside seq_chain,
-                            gn_points: transform + gathers + miss conversion, touched: the chunk loop, rays: step
-                            tail + its barrier, cells: the ingest prologue, updates: the level loop) -- tools/clk_match.py
   chainregs  WRONG RESULTS  hs_match_kernel's chain reads its first 16 terms from LDS and then re-adds the
                             registers it holds (same adds, no further LDS reads: prices the chain's LDS latency)
   noprio     same results   hs_match_kernel's chain wave stays at the default wave priority
-  dwordq     same results   hs_update_kernel loads and stores only the marked cells of a partially marked quad
-                            (4-byte accesses; whole quads stay 16-byte): prices the over-fetch of partial quads
   mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
                             streams per CU)
-  seq4acc    WRONG RESULTS  hs_match_kernel's sequential sum in 4 interleaved accumulators (same instruction
-                            count, a quarter of the dependency depth: latency vs issue)
 """
 import os
 import shutil
@@ -70,7 +57,6 @@ PATCHES = {
     "plain": [(K, "__device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) { atomicMin(p, ev); }",
                "__device__ __forceinline__ void upd_mark(unsigned *p, unsigned ev) "
                "{ *reinterpret_cast<volatile unsigned *>(p) = ev; }")],
-    "noapply": [(K, "        if (pend_tl) {\n", "        if (pend_tl && false) {\n")],
     "hwexp": [(K, "    float odds = sdm_expf_tab(l, s_exptab);", "    float odds = __expf(l);")],
     "gmplain": [("gmapping_kernels.hip", "        atomicAdd(reinterpret_cast<unsigned *>(pc), 1u); /* visits++ (:227-234) */ \\\n",
                  "        *reinterpret_cast<volatile unsigned *>(pc) = 1u;                             \\\n")],
@@ -80,8 +66,6 @@ PATCHES = {
                     '#define sdm_atan(x) ((double)atanf((float)(x)))\n')],
     "nowalk": [(K, "                    if ((int)!met | (int)(lo_i > hi_i)) continue;\n                    anyv = 1u;\n",
                 "                    if ((int)!met | (int)(lo_i > hi_i)) continue;\n                    anyv = 1u;\n                    continue;\n")],
-    "nosetup": [(K, "                        if (!((fm >> fi) & 1ull)) continue;\n",
-                 "                        if (!((fm >> fi) & 1ull)) continue;\n                        continue;\n")],
     "ktnorender": [("karto_kernels.hip", "kt_render_items_dw(tileb, sitem, c0, c1,", "kt_render_items_dw(tileb, sitem, c0, c0,")],
     "lds6": [("hector_capi.hip", "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points));\n}",
               "UPD_GROUP_WORDS * (size_t)fan_groups(c->max_points) + 2100);\n}")],
@@ -101,90 +85,13 @@ PATCHES = {
     "nohitbit": [(K, "                    atomicOr(&hitb[c >> 5], 1u << (c & 31));\n", "                    (void)c;\n")],
     "seqnochain": [(K, "        if (lane < 9) run = seq_chain(T, lane, cnt, run);",
                     "        if (lane < 9) run = run + T[lane * SEQ_STRIDE];")],
-    "seq4acc": [(K, "#define S2D_ADD4(v) do { run = run + (v).x; run = run + (v).y; run = run + (v).z; run = run + (v).w; } while (0)",
-                 "#define S2D_ADD4(v) do { run = run + (v).x; r1 = r1 + (v).y; r2 = r2 + (v).z; r3 = r3 + (v).w; } while (0)"),
-                (K, "    const float4 *row = reinterpret_cast<const float4 *>(T + lane * SEQ_STRIDE);\n    const int c4 = cnt >> 2;",
-                 "    const float4 *row = reinterpret_cast<const float4 *>(T + lane * SEQ_STRIDE);\n    const int c4 = cnt >> 2;\n    float r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;"),
-                (K, "    for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];\n    return run;",
-                 "    for (int r = 0; r < (cnt & 3); ++r) run = run + tail[r];\n    return run + (r1 + (r2 + r3));")],
     "frozen": [(K, "            for (int it = 0; it <= iters; ++it) {\n                if (in_regs) {",
                 "            for (int it = 0; it <= iters && false; ++it) {\n                if (in_regs) {")],
-    "noapplymath": [(K, "                    nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);",
-                     "                    nv[c] = t;")],
-    "fullstore": [(K, "                if ((mb & 15u) == 15u) {\n                    *reinterpret_cast<int4 *>(&tu[o])",
-                   "                if (true) {\n                    *reinterpret_cast<int4 *>(&tu[o])")],
-    "notiles": [(K, "    if (!__syncthreads_or(R != 0)) return;  // no ray drawn on this level\n",
-                 "    if (!__syncthreads_or(R != 0) || true) return;  // no ray drawn on this level\n")],
-    "clk": [(K, "    float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)\n",
-             "    float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)\n"
-             "    unsigned long long acc_r = 0, acc_a = 0, acc_b = 0, acc_m = 0;\n"),
-            (K, "    for (int i = 0; i <= my_tiles; ++i) {\n        const int t = part + i * parts;\n",
-             "    for (int i = 0; i <= my_tiles; ++i) {\n        const unsigned long long ck0 = clock64();\n        const int t = part + i * parts;\n"),
-            (K, "            if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);\n        }\n",
-             "            if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);\n        }\n"
-             "        const unsigned long long ck1 = clock64();\n"),
-            (K, "            pend_tl = nullptr;\n        }\n",
-             "            pend_tl = nullptr;\n        }\n        const unsigned long long ck2 = clock64();\n"
-             "        unsigned long long ck3 = ck2;\n"),
-            (K, "            lds_barrier();  // tile i's marks complete\n",
-             "            lds_barrier();  // tile i's marks complete\n            ck3 = clock64();\n"),
-            (K, "                    if ((tid & 7) == 0) hitb[row * (TILE / 32) + (c4 >> 5)] = 0u;\n                }\n            }\n        }\n    }\n",
-             "                    if ((tid & 7) == 0) hitb[row * (TILE / 32) + (c4 >> 5)] = 0u;\n                }\n            }\n        }\n"
-             "        const unsigned long long ck4 = clock64();\n"
-             "        acc_r += ck1 - ck0; acc_a += ck2 - ck1; acc_b += ck3 - ck2; acc_m += ck4 - ck3;\n    }\n"
-             "    if (lane == 0) {\n        atomicAdd(&state[s].tot_gn_points, acc_r); atomicAdd(&state[s].tot_updates, acc_a);\n"
-             "        atomicAdd(&state[s].tot_steps, acc_b); atomicAdd(&state[s].tot_touched, acc_m);\n    }\n")],
-    "mclk": [(K, "__device__ __forceinline__ void lds_barrier()\n",
-              "__shared__ unsigned long long s_mclk[8];\n__device__ __forceinline__ void lds_barrier()\n"),
-             (K, "        __builtin_amdgcn_s_setprio(3);\n        if (lane < 9) run = seq_chain(T, lane, cnt, run);\n",
-              "        __builtin_amdgcn_s_setprio(3);\n        __builtin_amdgcn_sched_barrier(0);\n"
-              "        const unsigned long long q0 = clock64();\n        __builtin_amdgcn_sched_barrier(0);\n"
-              "        if (lane < 9) run = seq_chain(T, lane, cnt, run);\n        __builtin_amdgcn_sched_barrier(0);\n"
-              "        const unsigned long long q1 = clock64();\n        __builtin_amdgcn_sched_barrier(0);\n"
-              "        if (lane == 0) s_mclk[0] += q1 - q0;\n"),
-             (K, "    const int tid = threadIdx.x;\n    PointFetch pf[NP];\n",
-              "    const int tid = threadIdx.x;\n    const unsigned long long mk0 = clock64();\n    PointFetch pf[NP];\n"),
-             (K, "    float run = 0.0f;                                       // SEQ: lane k < 9 of wave cw: sum of term k\n",
-              "    float run = 0.0f;                                       // SEQ: lane k < 9 of wave cw: sum of term k\n"
-              "    __builtin_amdgcn_sched_barrier(0);\n    const unsigned long long mk1 = clock64();\n    __builtin_amdgcn_sched_barrier(0);\n"),
-             (K, "    float *sp = s_pose[parity];\n    if (wave == cw) {\n",
-              "    __builtin_amdgcn_sched_barrier(0);\n    const unsigned long long mk2 = clock64();\n    __builtin_amdgcn_sched_barrier(0);\n"
-              "    float *sp = s_pose[parity];\n    if (wave == cw) {\n"),
-             (K, "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n",
-              "    __syncthreads();\n    {\n        const unsigned long long mk3 = clock64();\n"
-              "        if (SEQ && wave == cw && (tid & 63) == 0) { s_mclk[1] += mk1 - mk0; s_mclk[2] += mk2 - mk1; s_mclk[3] += mk3 - mk2; }\n"
-              "    }\n"
-              "    est[0] = sp[0];\n    est[1] = sp[1];\n"),
-             (K, "    load_exptab();\n    __syncthreads();\n    const float *scells",
-              "    const unsigned long long kk0 = clock64();\n    load_exptab();\n    if (threadIdx.x < 8) s_mclk[threadIdx.x] = 0;\n    __syncthreads();\n    const float *scells"),
-             (K, "        for (int lvl = geom.levels - 1; lvl >= 0; --lvl) {\n            const LevelGeom &g = geom.lv[lvl];\n            const int iters",
-              "        const unsigned long long kk1 = clock64();\n        if (threadIdx.x == 0) s_mclk[5] = kk1 - kk0;\n"
-              "        for (int lvl = geom.levels - 1; lvl >= 0; --lvl) {\n            const LevelGeom &g = geom.lv[lvl];\n            const int iters"),
-             (K, "        np_[0] = tmp[0];\n        np_[1] = tmp[1];\n        np_[2] = tmp[2];\n    }\n",
-              "        np_[0] = tmp[0];\n        np_[1] = tmp[1];\n        np_[2] = tmp[2];\n"
-              "        if (threadIdx.x == 0) s_mclk[6] = clock64() - kk1;\n    }\n"),
-             (K, "    if (threadIdx.x != 0) return;\n    if (local == 0) {",
-              "    __syncthreads();\n    if (threadIdx.x != 0) return;\n    if (local == 0) {"),
-             (K, "    st.tot_steps += 1;\n",
-              "    st.tot_steps += s_mclk[0];\n    st.tot_cells += s_mclk[5];\n    st.tot_rays += s_mclk[3];\n    st.tot_touched += s_mclk[2];\n"
-              "    st.tot_updates += s_mclk[6];\n"),
-             (K, "        st.tot_gn_points += it * (unsigned long long)n;\n", "        st.tot_gn_points += s_mclk[1];\n")],
     "chainregs": [(K, "            b0 = row[i]; b1 = row[i + 1]; b2 = row[i + 2]; b3 = row[i + 3];\n",
                    "            b0 = a0; b1 = a1; b2 = a2; b3 = a3;\n"),
                   (K, "            a0 = row[i + 4]; a1 = row[i + 5]; a2 = row[i + 6]; a3 = row[i + 7];\n", "")],
     "noprio": [(K, "        // it issues ahead of the co-resident workgroups' waves (s_setprio; back to 0 after the step tail)\n        __builtin_amdgcn_s_setprio(3);\n",
                 "        // it issues ahead of the co-resident workgroups' waves (s_setprio; back to 0 after the step tail)\n        __builtin_amdgcn_s_setprio(0);\n")],
-    "dwordq": [(K, "                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));\n",
-                "                    if (mk == 15u) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));\n"
-                "                    else if (mk) {\n"
-                "                        const float *qp = pend_tl + (unsigned)upd_off(row, c4, g.tiles_x);\n"
-                "                        if (mk & 1u) ql[j].x = qp[0];\n                        if (mk & 2u) ql[j].y = qp[1];\n"
-                "                        if (mk & 4u) ql[j].z = qp[2];\n                        if (mk & 8u) ql[j].w = qp[3];\n"
-                "                    }\n"),
-               (K, "                *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);\n",
-                "                if ((mb & 15u) == 15u) *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);\n"
-                "                else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n"
-                "                        if ((mb >> c) & 1u) pend_tl[o + (unsigned)c] = nv[c];\n                }\n")],
     "mlds3": [(K, "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n",
                "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n"
                "    __shared__ float s_pad[3000];\n    if (stream_begin < 0) s_pad[threadIdx.x] = 1.0f;\n")],
@@ -215,6 +122,22 @@ def build(variant: str) -> str:
         shutil.rmtree(tmp)
 
 
+def check() -> list:
+    """Variants whose patch anchors no longer occur exactly once in the sources (tests/test_host_cpu.py)."""
+    bad = []
+    for v, patches in sorted(PATCHES.items()):
+        for fname, old, _ in patches:
+            with open(os.path.join(PKG, "csrc", fname)) as f:
+                if f.read().count(old) != 1:
+                    bad.append(v)
+                    break
+    return bad
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["--check"]:
+        bad = check()
+        print("stale variants:", bad or "none")
+        sys.exit(1 if bad else 0)
     for v in sys.argv[1:]:
         print("built", build(v))

@@ -29,7 +29,7 @@ static inline float fat2(float y, float x, int m)
 }
 static double err_atan(float x, int m) { return fabs((double)fat(x, m) - atan((double)x)); }
 // the kernel's fast-path condition (pl_theta_cells) and the error against atan2 of the DOUBLE arguments
-static int fast2(float fy, float fx) { return fx != 0.0f && fy != 0.0f && fmaxf(fabsf(fx), fabsf(fy)) >= FLT_MIN; }
+static int fast2(float fy, float fx) { return fminf(fabsf(fx), fabsf(fy)) >= FLT_MIN; }  /* both components normal (pl_polar_cells) */
 static double err_atan2(double y, double x, int m)
 {
     float fx = (float)x, fy = (float)y;
@@ -98,6 +98,7 @@ int main(int argc, char **argv)
             case 4: x = y * 1e-30 * urand(); break;                       // huge ratio
             case 5: x = (urand() - 0.5) * 2.5e-38; y = (urand() - 0.5) * 2.5e-38; break;  // around FLT_MIN
             case 6: x = -fabs(x); y = copysign(1e-12 * fabs(x), (urand() < 0.5) ? -1.0 : 1.0); break;  // near +-pi
+            case 7: if (i % 16 == 7) y = (urand() - 0.5) * 2.0e-39; break;  // one subnormal component: exact path
             default: break;
             }
             double e = err_atan2(y, x, m);

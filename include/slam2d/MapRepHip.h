@@ -28,9 +28,14 @@
 #include <memory>
 #include <vector>
 
-#include "MapRepresentationInterface.h"      // lesson4/include/lesson4/hector_mapping/slam_main/
-#include "../map/GridMap.h"
+// Include order as HectorSlamProcessor.h:32-40: MapRepresentationInterface.h has no includes of its own and
+// forward-declares GridMap / DataContainer at global scope, so hectorslam::GridMap, DataContainer,
+// MapLockerInterface and Eigen must be declared before it, or its pure virtuals name other types than the
+// overrides below.
+#include "../map/GridMap.h"                  // -> Eigen, OccGridMapBase, DataPointContainer
 #include "../scan/DataPointContainer.h"
+#include "../util/MapLockerInterface.h"
+#include "MapRepresentationInterface.h"      // lesson4/include/lesson4/hector_mapping/slam_main/
 #include <slam2d/hector_map_backend.hpp>
 
 namespace hectorslam {

@@ -2426,6 +2426,46 @@ __device__ __forceinline__ void ring_split(int p, int parts, int kmax, int ox, i
     if (ke < kb) ke = kb;
 }
 
+// Weighted variant (default): ring k weighs RING_TILE_W per box tile plus one per ray that reaches it (the
+// rays' end rings are histogrammed in LDS, s_rh[RING_HIST]; rings past the last bin count in it).  Inner
+// rings hold few tiles but every ray's first steps, so a split by tiles alone left the inner part the
+// heaviest.  All threads call it (two block barriers); s_cut[2] receives [kb, ke).
+constexpr int RING_HIST = 128;
+#ifndef S2D_RING_SPLIT_TILES
+#define S2D_RING_SPLIT_TILES 0  // 1: split by tile count alone (A/B)
+#endif
+#ifndef S2D_RING_TILE_W
+#define S2D_RING_TILE_W 64
+#endif
+__device__ __forceinline__ void ring_split_w(int p, int parts, int kmax, int ox, int oy, int tx0, int tx1, int ty0,
+                                             int ty1, const unsigned *s_rh, int *s_wave, int *s_cut, int &kb, int &ke)
+{
+    const int tid = threadIdx.x;
+    // thread k: ring k's weight; rays reaching ring k = rays whose end ring is >= k
+    int w = 0;
+    if (tid <= kmax) {
+        const int kk = min(tid, RING_HIST - 1);
+        unsigned reach = 0;
+        for (int j = kk; j < RING_HIST; ++j) reach += s_rh[j];
+        const int tk = tiles_within(tid, ox, oy, tx0, tx1, ty0, ty1) - tiles_within(tid - 1, ox, oy, tx0, tx1, ty0, ty1);
+        w = S2D_RING_TILE_W * tk + (int)reach;
+    }
+    if (tid == 0) {
+        s_cut[0] = p == 0 ? 0 : kmax + 1;
+        s_cut[1] = kmax + 1;
+    }
+    int total;
+    const int before = block_exscan(w, s_wave, &total);  // weight of the rings < tid
+    const int lo = (int)(((long long)total * p) / parts), hi = (int)(((long long)total * (p + 1)) / parts);
+    if (tid >= 1 && tid <= kmax) {
+        if (p > 0 && before >= lo) atomicMin(&s_cut[0], tid);
+        if (p < parts - 1 && before >= hi) atomicMin(&s_cut[1], tid);
+    }
+    __syncthreads();
+    kb = s_cut[0];
+    ke = max(s_cut[1], kb);
+}
+
 // Next tile of the box in ring order: candidates (k, s, j), j = 0..7 the 8 tiles (+-k, +-s), (+-s, +-k),
 // duplicates skipped (s == 0: odd j; s == k: j >= 4; k == 0: j = 0 only).  The caller knows how many
 // tiles remain, so a candidate is always found.
@@ -2463,6 +2503,8 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
     extern __shared__ __attribute__((aligned(16))) unsigned smem[];
     __shared__ unsigned s_any[2];
     __shared__ unsigned s_touched;
+    __shared__ unsigned s_rh[RING_HIST];  // rays per end ring (ring_split_w)
+    __shared__ int s_wave[4], s_cut[2];
     int4 *gbox = reinterpret_cast<int4 *>(smem + UPD_FIXED_WORDS);  // per fan group: x0 y0 x1 y1
     const int lane = threadIdx.x & 63;
     __shared__ int s_bbox[4];
@@ -2498,12 +2540,14 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
     if (tid == 0) {
         s_bbox[0] = x0; s_bbox[1] = y0; s_bbox[2] = x0; s_bbox[3] = y0;
     }
+    if (tid < RING_HIST) s_rh[tid] = 0u;
     __syncthreads();
     int bx0 = x0, by0 = y0, bx1 = x0, by1 = y0;
     unsigned long long L = 0, R = 0;
     const float2 *pts = lvl == 0 ? xy + (size_t)local * xy_stride : mc + (size_t)s * mc_stride;
     const int wave_beam0 = __builtin_amdgcn_readfirstlane(tid & ~63);
     const int wave = wave_beam0 >> 6;
+    const int ox = x0 / TILE, oy = y0 / UPD_TH;  // the begin tile (x0, y0 >= 0 whenever a ray is valid)
     unsigned Ck[RING_GROUPS], Sk[RING_GROUPS];
 #pragma unroll
     for (int k = 0; k < RING_GROUPS; ++k) {
@@ -2519,6 +2563,10 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
             gx0 = min(gx0, x1); gy0 = min(gy0, y1); gx1 = max(gx1, x1); gy1 = max(gy1, y1);
             L += (unsigned long long)((Ck[k] & 0x3FFFu) + 1u);
             R += 1;
+            if (parts > 1) {
+                const int er = max(abs(x1 / TILE - ox), abs(y1 / UPD_TH - oy));
+                atomicAdd(&s_rh[min(er, RING_HIST - 1)], 1u);
+            }
         }
         bx0 = min(bx0, gx0); by0 = min(by0, gy0); bx1 = max(bx1, gx1); by1 = max(by1, gy1);
 #pragma unroll
@@ -2556,10 +2604,15 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
     }
     const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / UPD_TH;
     const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / UPD_TH;
-    const int ox = x0 / TILE, oy = y0 / UPD_TH;  // the begin tile (x0, y0 >= 0: valid rays start inside the map)
     const int kmax = max(max(ox - tx0, tx1 - ox), max(oy - ty0, ty1 - oy));
-    int kb, ke;
-    ring_split(part, parts, kmax, ox, oy, tx0, tx1, ty0, ty1, kb, ke);
+    int kb = 0, ke = kmax + 1;
+    if (parts > 1) {
+#if S2D_RING_SPLIT_TILES
+        ring_split(part, parts, kmax, ox, oy, tx0, tx1, ty0, ty1, kb, ke);
+#else
+        ring_split_w(part, parts, kmax, ox, oy, tx0, tx1, ty0, ty1, s_rh, s_wave, s_cut, kb, ke);
+#endif
+    }
     const int my_tiles = tiles_within(ke - 1, ox, oy, tx0, tx1, ty0, ty1) - tiles_within(kb - 1, ox, oy, tx0, tx1, ty0, ty1);
 #pragma unroll
     for (int k = 0; k < RING_GROUPS; ++k) Sk[k] = ray_cursor(Ck[k], kb, x0, y0, ox, oy);

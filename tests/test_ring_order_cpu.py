@@ -263,3 +263,31 @@ def test_ring_visits_mark_exactly_the_walk():
                     hits.append((tx * TILE + hc[0], ty * TH + hc[1]))
             assert free == cells[:-1] and hits == [cells[-1]], (trial, bwd, x0, y0, x1, y1)
             assert (S & 0xFFFF) == da + 1
+
+
+def ring_split_w(p, parts, kmax, ox, oy, box, hist, tile_w=64):
+    """ring_split_w (csrc/hector_kernels.hip): ring k weighs tile_w per box tile + the rays reaching it."""
+    w = []
+    for k in range(kmax + 1):
+        reach = sum(hist[min(k, len(hist) - 1):])
+        w.append(tile_w * (tiles_within(k, ox, oy, box) - tiles_within(k - 1, ox, oy, box)) + reach)
+    total = sum(w)
+    lo, hi = total * p // parts, total * (p + 1) // parts
+    before = np.concatenate([[0], np.cumsum(w)[:-1]])
+    kb = 0 if p == 0 else next((k for k in range(1, kmax + 1) if before[k] >= lo), kmax + 1)
+    ke = kmax + 1 if p == parts - 1 else next((k for k in range(1, kmax + 1) if before[k] >= hi), kmax + 1)
+    return kb, max(ke, kb)
+
+
+def test_weighted_ring_split_partitions_the_rings():
+    rng = np.random.default_rng(13)
+    for _ in range(400):
+        tx0, ty0 = (int(v) for v in rng.integers(0, 20, 2))
+        box = (tx0, tx0 + int(rng.integers(0, 15)), ty0, ty0 + int(rng.integers(0, 25)))
+        ox, oy = int(rng.integers(box[0], box[1] + 1)), int(rng.integers(box[2], box[3] + 1))
+        kmax = max(ox - box[0], box[1] - ox, oy - box[2], box[3] - oy)
+        hist = rng.integers(0, 200, 128) * (np.arange(128) <= kmax)
+        for parts in (2, 3, 8):
+            cuts = [ring_split_w(p, parts, kmax, ox, oy, box, hist) for p in range(parts)]
+            assert cuts[0][0] == 0 and cuts[-1][1] == kmax + 1
+            assert all(cuts[p][1] == cuts[p + 1][0] for p in range(parts - 1)), cuts

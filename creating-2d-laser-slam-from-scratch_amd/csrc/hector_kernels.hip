@@ -830,8 +830,8 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
         for (int j = 0; j < NP; ++j) {
             if (j >= nch) break;  // uniform
             const int slot = pt + j * CW_PTS;
+            float t[9];
             if (slot < n) {
-                float t[9];
                 PointFetch pf;  // the gather phase's transform, recomputed (the same operations, the same bits)
                 pf.px = p[j].x * f;
                 pf.py = p[j].y * f;
@@ -846,12 +846,14 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
                     pf.l[0] = v.x; pf.l[1] = v.y; pf.l[2] = v.z; pf.l[3] = v.w;
                 }
                 point_terms<true>(pf, cs, sn, t);
-                if (CW_BUFS == 1) lds_barrier();  // the chain wave is done with chunk j - 1 (j = 0: the miss lists)
+            }
+            // (barriers only in wave-uniform control flow: a wave whose lanes straddle n runs both sides of
+            // the slot test)
+            if (CW_BUFS == 1) lds_barrier();  // the chain wave is done with chunk j - 1 (j = 0: the miss lists)
+            if (slot < n) {
                 float *T = seqT + (CW_BUFS == 2 ? (j & 1) * CW_BUF : 0);
 #pragma unroll
                 for (int k = 0; k < 9; ++k) T[k * CW_STRIDE + pt] = t[k];
-            } else if (CW_BUFS == 1) {
-                lds_barrier();
             }
             lds_barrier();  // chunk j stored (two buffers: and the chain wave is done with chunk j - 1)
         }

@@ -269,12 +269,13 @@ bool upd_single_ok(const hs_ctx *c)
     return c->update_single && upd_shmem_bytes(c) <= 65536 && c->sx <= 16385 && c->sy <= 16385;
 }
 
+size_t ring_shmem_bytes(const hs_ctx *c) { return sizeof(unsigned) * (size_t)ring_shmem_words(c->max_points); }
+
 // hs_update_ring_kernel: rays in registers (<= RING_GROUPS * 256 points), da / db in 14 bits (<= 16384
 // cells per side)
 bool upd_ring_ok(const hs_ctx *c)
 {
-    return c->upd_ring && upd_rays_in_regs(c) && c->max_points <= RING_GROUPS * UPD_THREADS && c->sx <= 16384 &&
-           c->sy <= 16384;
+    return c->upd_ring && c->max_points <= 5 * 256 && c->sx <= 16384 && c->sy <= 16384;
 }
 
 int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int xy_stride, const int *n,
@@ -326,9 +327,9 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         c->wl_parity[part] ^= 1;
         begin_timed(c, 2, s);
         if (upd_ring_ok(c))
-            hipLaunchKernelGGL(hs_update_ring_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
-                               c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, wl_cur,
-                               wl_next, c->ncu);
+            hipLaunchKernelGGL(hs_update_ring_kernel, dim3(blocks), dim3(RTHREADS), ring_shmem_bytes(c), s, c->geom,
+                               c->d_cells, c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points,
+                               wl_cur, wl_next, c->ncu);
         else if (upd_rays_in_regs(c))
             hipLaunchKernelGGL((hs_update_kernel<UPD_RREG>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, c->geom, c->d_cells,
                                c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, wl_cur,
@@ -361,9 +362,9 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
         int blocks = 0;
         for (int l = 0; l < c->levels; ++l) blocks += gg.upd_parts[l] * count;
         if (upd_ring_ok(c))
-            hipLaunchKernelGGL(hs_update_ring_kernel, dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
-                               c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, (const UpdList *)nullptr,
-                               (UpdList *)nullptr, c->ncu);
+            hipLaunchKernelGGL(hs_update_ring_kernel, dim3(blocks), dim3(RTHREADS), ring_shmem_bytes(c), s, gg, c->d_cells,
+                               c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points,
+                               (const UpdList *)nullptr, (UpdList *)nullptr, c->ncu);
         else if (upd_rays_in_regs(c))
             hipLaunchKernelGGL((hs_update_kernel<UPD_RREG>), dim3(blocks), dim3(UPD_THREADS), upd_shmem, s, gg, c->d_cells,
                                c->d_state, xy, xy_stride, c->d_ixy, c->max_points, begin, count, c->max_points, (const UpdList *)nullptr,

@@ -2274,7 +2274,31 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
 //   consts  = da | db << 14 | (x step < 0) << 28 | (y step < 0) << 29 | x major << 30   (0: no ray)
 //   cursor  = i | q << 16: step i is next, q = its minor steps (i > da: the ray is done)
 // (da, db < 2^14: maps of at most 16384 cells per side, upd_ring_ok).
-constexpr int RING_GROUPS = 5;
+// LDS tile height of the ring kernel: 32 rows with 256-thread workgroups (default), or 64 rows with 512-thread
+// workgroups (S2D_RING_TH=64: a ray crosses fewer tiles; the same LDS and registers per wave, 2 quads per
+// thread in the apply, 8 waves at every tile barrier)
+#ifndef S2D_RING_TH
+#define S2D_RING_TH 32
+#endif
+constexpr int RTH = S2D_RING_TH;
+constexpr int RTHREADS = RTH == 64 ? 512 : 256;
+constexpr int RWAVES = RTHREADS / 64;
+static_assert(RTH % TILE_H == 0 && (RTH == 32 || RTH == 64), "ring tiles: 32 or 64 rows");
+constexpr int RTILE_WORDS = RTH * UPD_STRIDE;                       // one LDS mark array
+constexpr int RHIT_WORDS = RTH * (TILE / 32);                       // one hit bit per tile cell
+constexpr int RMARK_WORDS = (RTILE_WORDS + RHIT_WORDS + 3) & ~3;
+constexpr int RFIXED_WORDS = 2 * RMARK_WORDS + 4;                  // two mark buffers + 4 spare words; then fan boxes
+constexpr int RQUADS = TILE * RTH / 4 / RTHREADS;                   // apply quads per thread per tile
+constexpr unsigned long long RGROUP_MASK = RWAVES == 4 ? 0x1111111111111111ull : 0x0101010101010101ull;
+constexpr int RING_GROUPS = (5 * 256 + RTHREADS - 1) / RTHREADS;    // fan groups per lane: scans of <= 1280 points
+__host__ __device__ constexpr int ring_fan_groups(int max_points) { return ((max_points + RTHREADS - 1) / RTHREADS) * RWAVES; }
+__host__ __device__ constexpr int ring_shmem_words(int max_points) { return RFIXED_WORDS + UPD_GROUP_WORDS * ring_fan_groups(max_points); }
+// word offset of the quad at (c4, row) of the LDS tile in the level's tiled storage (see upd_off)
+__device__ __forceinline__ int ring_off(int row, int c4, int tiles_x)
+{
+    if constexpr (RTH == TILE_H) return tile_cell(c4, row);
+    return (row / TILE_H) * tiles_x * TILE_BLOCK_WORDS + tile_cell(c4, row % TILE_H);
+}
 constexpr unsigned CUR_DONE = 0xFFFFu;
 
 __device__ __forceinline__ unsigned ray_consts(int x0, int y0, unsigned r)
@@ -2307,7 +2331,7 @@ __device__ __forceinline__ unsigned ray_cursor(unsigned C, int K, int x0, int y0
     const bool sxn = (C >> 28) & 1u, syn = (C >> 29) & 1u, xm = (C >> 30) & 1u;
     const int e0 = da >> 1;
     const int Dx = sxn ? x0 - ((ox - K) * TILE + TILE - 1) : (ox + K) * TILE - x0;
-    const int Dy = syn ? y0 - ((oy - K) * UPD_TH + UPD_TH - 1) : (oy + K) * UPD_TH - y0;
+    const int Dy = syn ? y0 - ((oy - K) * RTH + RTH - 1) : (oy + K) * RTH - y0;
     const int INF = 0x7FFF;
     const int Dma = xm ? Dx : Dy, Dmi = xm ? Dy : Dx;
     const int im = Dma <= da ? Dma : INF;
@@ -2337,9 +2361,9 @@ __device__ __forceinline__ void ring_visit(unsigned C, unsigned &S, unsigned b, 
     const int ix = xm ? i : q, iy = xm ? q : i;
     const int lx = rx0 + ((ix ^ mx) - mx), ly = ry0 + ((iy ^ my) - my);
     // done rays (i > da) and cursors outside the tile: nothing here (one branch)
-    if ((int)(i > da) | (int)((unsigned)lx >= (unsigned)TILE) | (int)((unsigned)ly >= (unsigned)UPD_TH)) return;
+    if ((int)(i > da) | (int)((unsigned)lx >= (unsigned)TILE) | (int)((unsigned)ly >= (unsigned)RTH)) return;
     // steps after this one that stay inside the tile along x / y
-    const int rx = lx ^ ((TILE - 1) & ~mx), ry = ly ^ ((UPD_TH - 1) & ~my);
+    const int rx = lx ^ ((TILE - 1) & ~mx), ry = ly ^ ((RTH - 1) & ~my);
     const int ra = xm ? rx : ry, rb = xm ? ry : rx;
     const int e = (da >> 1) + (int)__umul24((unsigned)i, (unsigned)db) - (int)__umul24((unsigned)q, (unsigned)da);
     // steps inside the tile, this one included: the major axis leaves after ra + 1, the walk ends at step
@@ -2428,6 +2452,30 @@ __device__ __forceinline__ void ring_split(int p, int parts, int kmax, int ox, i
     if (ke < kb) ke = kb;
 }
 
+// block-wide exclusive scan over the ring kernel's RTHREADS threads (s_wave: RWAVES ints)
+__device__ __forceinline__ int ring_exscan(int v, int *s_wave, int *total)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(x, off, 64);
+        if (lane >= off) x += t;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < RWAVES; ++k) {
+        const int ws = s_wave[k];
+        if (k < wave) base += ws;
+        tot += ws;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
 // Weighted variant (default): ring k weighs RING_TILE_W per box tile plus one per ray that reaches it (the
 // rays' end rings are histogrammed in LDS, s_rh[RING_HIST]; rings past the last bin count in it).  Inner
 // rings hold few tiles but every ray's first steps, so a split by tiles alone left the inner part the
@@ -2457,7 +2505,7 @@ __device__ __forceinline__ void ring_split_w(int p, int parts, int kmax, int ox,
         s_cut[1] = kmax + 1;
     }
     int total;
-    const int before = block_exscan(w, s_wave, &total);  // weight of the rings < tid
+    const int before = ring_exscan(w, s_wave, &total);  // weight of the rings < tid
     const int lo = (int)(((long long)total * p) / parts), hi = (int)(((long long)total * (p + 1)) / parts);
     if (tid >= 1 && tid <= kmax) {
         if (p > 0 && before >= lo) atomicMin(&s_cut[0], tid);
@@ -2496,7 +2544,7 @@ struct RingIter {
     }
 };
 
-__global__ void __launch_bounds__(UPD_THREADS, S2D_UPD_MINB)
+__global__ void __launch_bounds__(RTHREADS, S2D_UPD_MINB * 256 / RTHREADS)
 hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restrict__ state,
                       const float2 *__restrict__ xy, int xy_stride, const float2 *__restrict__ mc, int mc_stride,
                       int stream_begin, int count, int max_points, const UpdList *__restrict__ wl,
@@ -2506,8 +2554,8 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
     __shared__ unsigned s_any[2];
     __shared__ unsigned s_touched;
     __shared__ unsigned s_rh[RING_HIST];  // rays per end ring (ring_split_w)
-    __shared__ int s_wave[4], s_cut[2];
-    int4 *gbox = reinterpret_cast<int4 *>(smem + UPD_FIXED_WORDS);  // per fan group: x0 y0 x1 y1
+    __shared__ int s_wave[RWAVES], s_cut[2];
+    int4 *gbox = reinterpret_cast<int4 *>(smem + RFIXED_WORDS);  // per fan group: x0 y0 x1 y1
     const int lane = threadIdx.x & 63;
     __shared__ int s_bbox[4];
 
@@ -2549,13 +2597,13 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
     const float2 *pts = lvl == 0 ? xy + (size_t)local * xy_stride : mc + (size_t)s * mc_stride;
     const int wave_beam0 = __builtin_amdgcn_readfirstlane(tid & ~63);
     const int wave = wave_beam0 >> 6;
-    const int ox = x0 / TILE, oy = y0 / UPD_TH;  // the begin tile (x0, y0 >= 0 whenever a ray is valid)
+    const int ox = x0 / TILE, oy = y0 / RTH;  // the begin tile (x0, y0 >= 0 whenever a ray is valid)
     unsigned Ck[RING_GROUPS], Sk[RING_GROUPS];
 #pragma unroll
     for (int k = 0; k < RING_GROUPS; ++k) {
         Ck[k] = 0u;
-        const int b0 = wave_beam0 + k * UPD_THREADS;
-        if ((b0 & ~255) >= n) continue;  // uniform: every group of a started 256-beam block gets its box
+        const int b0 = wave_beam0 + k * RTHREADS;
+        if ((b0 & ~(RTHREADS - 1)) >= n) continue;  // uniform: every group of a started block gets its box
         const int b = fan_beam(b0, lane);
         const unsigned r = b < n ? make_ray(g, fr, pts[b]) : RAY_INVALID;
         Ck[k] = ray_consts(x0, y0, r);
@@ -2566,11 +2614,10 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
             L += (unsigned long long)((Ck[k] & 0x3FFFu) + 1u);
             R += 1;
             if (parts > 1) {
-                const int er = max(abs(x1 / TILE - ox), abs(y1 / UPD_TH - oy));
+                const int er = max(abs(x1 / TILE - ox), abs(y1 / RTH - oy));
                 atomicAdd(&s_rh[min(er, RING_HIST - 1)], 1u);
             }
         }
-        bx0 = min(bx0, gx0); by0 = min(by0, gy0); bx1 = max(bx1, gx1); by1 = max(by1, gy1);
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
             gx0 = min(gx0, __shfl_xor(gx0, off, 64));
@@ -2578,24 +2625,27 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
             gx1 = max(gx1, __shfl_xor(gx1, off, 64));
             gy1 = max(gy1, __shfl_xor(gy1, off, 64));
         }
+        // the wave's box from its (wave-uniform) group boxes
+        bx0 = min(bx0, gx0); by0 = min(by0, gy0); bx1 = max(bx1, gx1); by1 = max(by1, gy1);
         if (lane == 0) gbox[b0 >> 6] = make_int4(gx0, gy0, gx1, gy1);
-    }
-    if (R) {
-        atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
-        atomicMax(&s_bbox[2], bx1); atomicMax(&s_bbox[3], by1);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         L += __shfl_xor(L, off, 64);
         R += __shfl_xor(R, off, 64);
     }
+    // one lane per wave: per-lane atomics here compiled to a scalar loop over the active lanes per word
+    if (lane == 0 && R) {
+        atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
+        atomicMax(&s_bbox[2], bx1); atomicMax(&s_bbox[3], by1);
+    }
     if (lane == 0 && R && part == 0) {
         atomicAdd(&state[s].step_cells, L);
         atomicAdd(&state[s].tot_cells, L);
         atomicAdd(&state[s].tot_rays, R);
     }
-    for (int k = tid; k < 2 * UPD_MARK_WORDS / 4; k += UPD_THREADS)
-        reinterpret_cast<uint4 *>(smem)[k] = (k % (UPD_MARK_WORDS / 4)) < UPD_TILE_WORDS / 4
+    for (int k = tid; k < 2 * RMARK_WORDS / 4; k += RTHREADS)
+        reinterpret_cast<uint4 *>(smem)[k] = (k % (RMARK_WORDS / 4)) < RTILE_WORDS / 4
                                                  ? make_uint4(W_NONE, W_NONE, W_NONE, W_NONE)
                                                  : make_uint4(0u, 0u, 0u, 0u);
     if (tid < 2) s_any[tid] = 0u;
@@ -2604,8 +2654,8 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
         clk_stamp(geom.clk, 1, false);
         return;
     }
-    const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / UPD_TH;
-    const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / UPD_TH;
+    const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / RTH;
+    const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / RTH;
     const int kmax = max(max(ox - tx0, tx1 - ox), max(oy - ty0, ty1 - oy));
     int kb = 0, ke = kmax + 1;
     if (parts > 1) {
@@ -2622,7 +2672,7 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
     const int mark_occ = st.mark_base + 2;   // currMarkOccIndex  (:121)
     const float lf = geom.lf, lo = geom.lo;
     unsigned touched = 0;
-    const int nfans = ((n + UPD_THREADS - 1) / UPD_THREADS) * (UPD_THREADS / 64);
+    const int nfans = ((n + RTHREADS - 1) / RTHREADS) * (RTHREADS / 64);
     const int bm = -(lane & 1);  // odd lanes (bm = -1) walk their segments backwards (see hs_update_kernel)
     RingIter it;
     it.k = kb;
@@ -2630,19 +2680,19 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
     it.j = -1;
     it.ox = ox; it.oy = oy; it.tx0 = tx0; it.tx1 = tx1; it.ty0 = ty0; it.ty1 = ty1;
 
-    float4 ql[UPD_QUADS];
-    unsigned qb[UPD_QUADS];
+    float4 ql[RQUADS];
+    unsigned qb[RQUADS];
     float *pend_tl = nullptr;
     for (int ii = 0; ii <= my_tiles; ++ii) {
         const int i = __builtin_amdgcn_readfirstlane(ii);
         const int buf = i & 1;
-        unsigned *marks = smem + buf * UPD_MARK_WORDS;
-        unsigned *hitb = marks + UPD_TILE_WORDS;
+        unsigned *marks = smem + buf * RMARK_WORDS;
+        unsigned *hitb = marks + RTILE_WORDS;
         int tx = 0, ty = 0;
         if (i < my_tiles) {
             it.next(tx, ty);
-            const int X0 = tx * TILE, Y0 = ty * UPD_TH;
-            const int X1 = X0 + TILE, Y1 = Y0 + UPD_TH;
+            const int X0 = tx * TILE, Y0 = ty * RTH;
+            const int X1 = X0 + TILE, Y1 = Y0 + RTH;
             unsigned anyv = 0u;
             unsigned long long fm;
             {
@@ -2655,27 +2705,22 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
             const int rx0 = x0 - X0, ry0 = y0 - Y0;
             // this wave's groups (fi = wave + 4 k) that meet the tile, one set bit each (scalar find-first-set);
             // the visit exists once, its group's two registers picked and written back by scalar branches
-            unsigned long long gm = fm & (0x1111111111111111ull << wave);
+            unsigned long long gm = fm & (RGROUP_MASK << wave);
             while (gm) {
-                const int k = __builtin_ctzll(gm) >> 2;
+                const int k = __builtin_ctzll(gm) / RWAVES;
                 gm &= gm - 1ull;
-                unsigned C, S;
-                switch (k) {
-                case 0: C = Ck[0]; S = Sk[0]; break;
-                case 1: C = Ck[1]; S = Sk[1]; break;
-                case 2: C = Ck[2]; S = Sk[2]; break;
-                case 3: C = Ck[3]; S = Sk[3]; break;
-                default: C = Ck[4]; S = Sk[4]; break;
-                }
-                const unsigned b = (unsigned)fan_beam(wave_beam0 + k * UPD_THREADS, lane);
+                unsigned C = Ck[0], S = Sk[0];
+#pragma unroll
+                for (int kk = 1; kk < RING_GROUPS; ++kk)
+                    if (k == kk) {
+                        C = Ck[kk];
+                        S = Sk[kk];
+                    }
+                const unsigned b = (unsigned)fan_beam(wave_beam0 + k * RTHREADS, lane);
                 ring_visit(C, S, b, rx0, ry0, marks, hitb, anyv, bm);
-                switch (k) {
-                case 0: Sk[0] = S; break;
-                case 1: Sk[1] = S; break;
-                case 2: Sk[2] = S; break;
-                case 3: Sk[3] = S; break;
-                default: Sk[4] = S; break;
-                }
+#pragma unroll
+                for (int kk = 0; kk < RING_GROUPS; ++kk)
+                    if (k == kk) Sk[kk] = S;
             }
             if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);
         }
@@ -2687,11 +2732,11 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
             int tq = tid;
             asm volatile("" : "+v"(tq));
 #pragma unroll
-            for (int j = 0; j < UPD_QUADS; ++j) {
+            for (int j = 0; j < RQUADS; ++j) {
                 const unsigned mb = qb[j];
                 if (!(mb & 15u)) continue;
-                const int qi = tq + j * UPD_THREADS;
-                const unsigned o = (unsigned)upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
+                const int qi = tq + j * RTHREADS;
+                const unsigned o = (unsigned)ring_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
@@ -2721,12 +2766,12 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
         if (i < my_tiles) {
             lds_barrier();  // tile i's marks complete
             if (s_any[buf] == (unsigned)(i + 1)) {
-                pend_tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
+                pend_tl = lvw + (size_t)(tx + ty * (RTH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
                 int tq = tid;
                 asm volatile("" : "+v"(tq));
 #pragma unroll
-                for (int j = 0; j < UPD_QUADS; ++j) {
-                    const unsigned qi = (unsigned)tq + j * UPD_THREADS;
+                for (int j = 0; j < RQUADS; ++j) {
+                    const unsigned qi = (unsigned)tq + j * RTHREADS;
                     const int row = (int)(qi >> 4), c4 = (int)((qi & 15u) << 2);
                     const int mw = lds_row(row) + c4;
                     const uint4 m = *reinterpret_cast<const uint4 *>(&marks[mw]);
@@ -2735,7 +2780,7 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
                                         ((unsigned)(m.z != W_NONE) << 2) | ((unsigned)(m.w != W_NONE) << 3);
                     const unsigned od = (m.x & 1u) | ((m.y & 1u) << 1) | ((m.z & 1u) << 2) | ((m.w & 1u) << 3);
                     qb[j] = mk | ((od & mk) << 4) | ((h & mk) << 8);
-                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));
+                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)ring_off(row, c4, g.tiles_x));
                     if (mk) {
                         // "no mark" from an opaque register: a hoisted all-ones quad was held across the loop
                         // and spilled (its reload waited for the quad loads just issued)

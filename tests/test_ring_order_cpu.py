@@ -8,6 +8,7 @@ OccGridMapBase.h:220-299 -- and if the enumeration yields every tile of the box 
 checked here on random rays and boxes (64 x 32-cell tiles, as the kernel's LDS tiles).
 """
 import numpy as np
+import pytest
 
 TILE, TH = 64, 32
 
@@ -94,7 +95,16 @@ def ring_split(p, parts, kmax, ox, oy, box):
     return kb, max(ke, kb)
 
 
-def test_every_ray_meets_its_tiles_in_ring_order():
+@pytest.fixture(params=[32, 64], ids=["th32", "th64"])
+def tile_h(request):
+    """The ring kernel's LDS tile height (S2D_RING_TH: 32 with 256-thread workgroups, 64 with 512)."""
+    global TH
+    old, TH = TH, request.param
+    yield request.param
+    TH = old
+
+
+def test_every_ray_meets_its_tiles_in_ring_order(tile_h):
     rng = np.random.default_rng(7)
     for _ in range(3000):
         x0, y0 = (int(v) for v in rng.integers(0, 2048, 2))
@@ -156,7 +166,7 @@ def ray_cursor(x0, y0, x1, y1, K, ox, oy):
     return i, (e0 + i * db) // da
 
 
-def test_ray_cursor_is_the_first_step_in_the_ring():
+def test_ray_cursor_is_the_first_step_in_the_ring(tile_h):
     rng = np.random.default_rng(3)
     for _ in range(3000):
         x0, y0 = (int(v) for v in rng.integers(0, 2048, 2))
@@ -232,7 +242,7 @@ def ring_visit(C, S, rx0, ry0, bwd):
     return Sn, cells, hitcell
 
 
-def test_ring_visits_mark_exactly_the_walk():
+def test_ring_visits_mark_exactly_the_walk(tile_h):
     """Every ray, visited tile by tile in ring order through ring_visit (forward and backward lanes), marks
     exactly the cells of its Bresenham walk: steps 0..da-1 free, step da the end cell."""
     rng = np.random.default_rng(5)

@@ -2741,15 +2741,25 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
                 int uv[4];
+                if (!__any((mb >> 8) & 15u)) {
+                    // no end cell in this quad slot of the whole wave (three quarters of level 0's, tools'
+                    // density model): every marked cell is free only -- updateSetFree alone
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float l = lv[c];
-                    const float t = l + lf;                       // updateSetFree
-                    const float u = t - lf;                       // ... then updateUnsetFree
-                    const float h = bit_select(mb, 4 + c, u, l);  // an earlier beam freed the hit cell
-                    const float oc = h < 50.0f ? h + lo : h;      // updateSetOccupied
-                    nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);
-                    uv[c] = __float_as_int(bit_select(mb, 8 + c, __int_as_float(mark_occ), __int_as_float(mark_free)));
+                    for (int c = 0; c < 4; ++c) {
+                        nv[c] = bit_select(mb, c, lv[c] + lf, lv[c]);
+                        uv[c] = mark_free;
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const float l = lv[c];
+                        const float t = l + lf;                       // updateSetFree
+                        const float u = t - lf;                       // ... then updateUnsetFree
+                        const float h = bit_select(mb, 4 + c, u, l);  // an earlier beam freed the hit cell
+                        const float oc = h < 50.0f ? h + lo : h;      // updateSetOccupied
+                        nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);
+                        uv[c] = __float_as_int(bit_select(mb, 8 + c, __int_as_float(mark_occ), __int_as_float(mark_free)));
+                    }
                 }
                 *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);
                 if ((mb & 15u) == 15u) {

@@ -19,7 +19,7 @@ timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/driver_cm
   || { echo "FAIL bench"; tail -20 $O/driver_cmd.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/driver_cmd.json'));r=d['roofline'];print('value',d['value'],'ms',d['ms_per_step'],'kms',r['kernel_ms_per_step'],'sclk',r.get('update_sclk_mhz'),r.get('match_sclk_mhz'),'pose',d['pose_vs_ref']['exact_frac_vs_reference_order'])"
 BENCH_ARGS="--steps 20 --warmup 5" timeout -k 10 900 bash tools/ab_bench.sh $T main main+SLAM2D_UPD_KERNEL=clip th64 cw1 || exit 1
-BENCH_ARGS="--steps 20 --warmup 5 --streams 2560" timeout -k 10 600 bash tools/ab_bench.sh ${T}_2560 main cw1 || exit 1
+BENCH_ARGS="--steps 20 --warmup 5 --streams 2560" timeout -k 10 600 bash tools/ab_bench.sh ${T}_2560 cw1 th64cw1 || exit 1
 BENCH_DIST_BACKEND=gloo timeout -k 10 300 python3 bench.py --gpus 2 --streams 512 --no-cpu-baseline --steps 10 \
   > $O/n2_northstar.json 2> $O/n2_northstar.err || { echo "FAIL n2 northstar"; tail -20 $O/n2_northstar.err; exit 1; }
 BENCH_DIST_BACKEND=gloo timeout -k 10 300 python3 bench.py --gpus 2 --config gmapping --weights torch --no-cpu-baseline \

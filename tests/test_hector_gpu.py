@@ -551,3 +551,63 @@ def test_batch_sizes_across_split_rules(gpu, B):
             ol, ou = oras[s].level(lvl)
             np.testing.assert_array_equal(m["upd"], ou)
             np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))
+
+
+@pytest.mark.parametrize("split", ["", "1,1,1", "6,3,2"])
+def test_ring_kernel_equals_clip_kernel(gpu, monkeypatch, split):
+    """The round-4 ring-ordered cursor update (default) and round 3's per-tile clipping kernel
+    (SLAM2D_UPD_KERNEL=clip) on the same 96-stream fleet, 4 steps, 2048^2 x 3 levels: every stream's pose and
+    every cell of sampled streams identical -- including ring-range parts (SLAM2D_UPD_SPLIT)."""
+    import torch
+
+    B, T = 96, 4
+    S = synth.make_streams(B, T, seed=31)
+    if split:
+        monkeypatch.setenv("SLAM2D_UPD_SPLIT", split)
+    fleets = {}
+    for kern in ("ring", "clip"):
+        if kern == "clip":
+            monkeypatch.setenv("SLAM2D_UPD_KERNEL", "clip")
+        f = HectorFleet(B, 0.05, 2048, (0.5, 0.5), 3, max_points=1081)
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(-1.0, -1.0)
+        fleets[kern] = f
+    monkeypatch.delenv("SLAM2D_UPD_KERNEL", raising=False)
+    for t in range(T):
+        d_xy = _torch_dev(S.points[:, t])
+        d_n = _torch_dev(S.counts[:, t].astype(np.int32))
+        for f in fleets.values():
+            f.step_device(d_xy.data_ptr(), 1081, d_n.data_ptr())
+        torch.cuda.synchronize()
+        pr, pc = fleets["ring"].poses()[0], fleets["clip"].poses()[0]
+        np.testing.assert_array_equal(_bits(pr), _bits(pc), err_msg=f"step {t}")
+    cr, cc = fleets["ring"].counters(reset=False), fleets["clip"].counters(reset=False)
+    assert cr["cells"] == cc["cells"] and cr["touched"] == cc["touched"], (cr, cc)
+    for s in (0, 47, B - 1):
+        for lvl in range(3):
+            mr, mc = fleets["ring"].get_map(s, lvl), fleets["clip"].get_map(s, lvl)
+            np.testing.assert_array_equal(mr["upd"], mc["upd"], err_msg=f"s={s} lvl={lvl}")
+            np.testing.assert_array_equal(_bits(mr["logodds"]), _bits(mc["logodds"]), err_msg=f"s={s} lvl={lvl}")
+
+
+def test_clock_probe(gpu):
+    """hs_set_clock_probe: the sampled workgroups of both kernels report a plausible shader clock."""
+    import torch
+
+    B = 64
+    S = synth.make_streams(B, 3, seed=5)
+    fleet = HectorFleet(B, 0.05, 1024, (0.5, 0.5), 2, max_points=1081)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(-1.0, -1.0)
+    fleet.set_clock_probe(True)
+    fleet.clock_probe(reset=True)
+    for t in range(3):
+        d_xy = _torch_dev(S.points[:, t])
+        d_n = _torch_dev(S.counts[:, t].astype(np.int32))
+        fleet.step_device(d_xy.data_ptr(), 1081, d_n.data_ptr())
+    torch.cuda.synchronize()
+    c = fleet.clock_probe(reset=True)
+    fleet.set_clock_probe(False)
+    for k in ("match", "update"):
+        assert c[k]["workgroups_sampled"] > 0, c
+        assert 300.0 < c[k]["sclk_mhz"] < 3000.0, c

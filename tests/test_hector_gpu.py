@@ -282,7 +282,8 @@ def test_long_rays_over_16384_cells(gpu):
     kernel's packed walk holds the Bresenham error in 14 bits, so the host sends such maps to the binned
     kernels (upd_single_ok); the result must still equal the oracle cell for cell."""
     sx, sy = 16640, 64
-    pts = [(821.7, 0.3), (821.7, -1.2), (700.0, 0.9), (-5.0, 0.2), (3.0, 1.0), (0.5, -1.5)]
+    # DataContainer points are in map scale (cells of level 0, hector_slam.cc:356): 16434 cells = 821.7 m
+    pts = [(16434.0, 6.0), (16434.0, -24.0), (14000.0, 18.0), (-100.0, 4.0), (60.0, 20.0), (10.0, -30.0)]
     pts = np.asarray(pts, np.float32)
     fleet = HectorFleet(1, 0.05, sx, (0.01, 0.5), 2, max_points=len(pts), map_size_y=sy)
     ora = O.HectorOracle(0.05, sx, (0.01, 0.5), 2, reduce_threads=T_RED, map_size_y=sy)

@@ -86,9 +86,9 @@ struct hs_ctx {
     // least 2 when the pipelined run (SLAM2D_PIPELINE=1) drives the two fleet halves as parts 0 and 1
     int nq = 1;
     int update_single = 1;  // hs_update_kernel (per stream-level, default) or bin + tile kernels
-    // the single-kernel update: hs_update_ring_kernel (ring-ordered tiles, ray cursors; default) or the
-    // round-3 hs_update_kernel (per-tile clipping; SLAM2D_UPD_KERNEL=clip, and scans of > 1280 points)
-    bool upd_ring = true;
+    // the single-kernel update: the round-3 hs_update_kernel (per-tile clipping; default) or
+    // hs_update_ring_kernel (ring-ordered tiles, ray cursors; SLAM2D_UPD_KERNEL=ring, scans of <= 1280 points)
+    bool upd_ring = false;
     int ncu = 256;
     bool upd_parts_fixed = false;  // SLAM2D_UPD_PARTS given: no batch-size adaptive split
     // per part (a batch split over part streams): two alternating lists of updating streams
@@ -563,8 +563,10 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         c->nparts = np ? atoi(np) : 1;
         const char *um = getenv("SLAM2D_UPDATE");
         c->update_single = (um && strcmp(um, "binned") == 0) ? 0 : 1;  // measured: single 1.06 ms vs binned 1.30 ms
+        // measured (round 4, profiles/r04/ab_r04c.md): ring 1.084 ms vs clip 0.924 ms per 2048-stream launch --
+        // the ring kernel's cursors save little VALU and its tile enumeration costs SALU; opt-in only
         const char *uk = getenv("SLAM2D_UPD_KERNEL");
-        c->upd_ring = !(uk && strcmp(uk, "clip") == 0);
+        c->upd_ring = uk && strcmp(uk, "ring") == 0;
         // workgroups per (stream, level) of hs_update_kernel: adaptive (launch_part: 1 at >= 512 streams,
         // where splitting measured neutral to slower), or fixed by SLAM2D_UPD_PARTS="p0,p1,..." 
         for (int l = 0; l < MAX_LEVELS; ++l) c->geom.upd_parts[l] = 1;

@@ -1788,6 +1788,9 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
 // no stride changes -- tools/lds_sim.py: 2 % fewer raster LDS cycles -- and the unaligned quads cost the
 // apply more: measured 0.005 ms slower.)
 constexpr int UPD_STRIDE = S2D_UPD_STRIDE;
+#ifndef S2D_APPLY_FAST
+#define S2D_APPLY_FAST 1  // 0: every marked quad takes the full apply_cell sequence (A/B)
+#endif
 #ifndef S2D_UPD_TH
 #define S2D_UPD_TH 32
 #endif
@@ -2191,18 +2194,28 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
                 int uv[4];
-                // apply_cell on the 4 cells without branches: every candidate value computed, then picked by
-                // bit selects on the sign-extended mark bits (v_bfe_i32 + v_bfi_b32: two VALU per choice; the
-                // branchy form compiled to exec-mask code around each cell)
+                if (S2D_APPLY_FAST && !__any((mb >> 8) & 15u)) {
+                    // no end cell in this quad slot of the whole wave (about three quarters of level 0's on the
+                    // synthetic scans): every marked cell is free only -- updateSetFree alone, two VALU per cell
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float l = lv[c];
-                    const float t = l + lf;                       // updateSetFree
-                    const float u = t - lf;                       // ... then updateUnsetFree
-                    const float h = bit_select(mb, 4 + c, u, l);  // an earlier beam freed the hit cell
-                    const float oc = h < 50.0f ? h + lo : h;      // updateSetOccupied
-                    nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);
-                    uv[c] = __float_as_int(bit_select(mb, 8 + c, __int_as_float(mark_occ), __int_as_float(mark_free)));
+                    for (int c = 0; c < 4; ++c) {
+                        nv[c] = bit_select(mb, c, lv[c] + lf, lv[c]);
+                        uv[c] = mark_free;
+                    }
+                } else {
+                    // apply_cell on the 4 cells without branches: every candidate value computed, then picked by
+                    // bit selects on the sign-extended mark bits (v_bfe_i32 + v_bfi_b32: two VALU per choice; the
+                    // branchy form compiled to exec-mask code around each cell)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const float l = lv[c];
+                        const float t = l + lf;                       // updateSetFree
+                        const float u = t - lf;                       // ... then updateUnsetFree
+                        const float h = bit_select(mb, 4 + c, u, l);  // an earlier beam freed the hit cell
+                        const float oc = h < 50.0f ? h + lo : h;      // updateSetOccupied
+                        nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);
+                        uv[c] = __float_as_int(bit_select(mb, 8 + c, __int_as_float(mark_occ), __int_as_float(mark_free)));
+                    }
                 }
                 // log-odds: the whole quad was loaded, so it is stored whole (one instruction; unmarked
                 // cells rewrite their own value); updateIndex: whole when every cell is marked, else
@@ -2741,7 +2754,7 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
                 int uv[4];
-                if (!__any((mb >> 8) & 15u)) {
+                if (S2D_APPLY_FAST && !__any((mb >> 8) & 15u)) {
                     // no end cell in this quad slot of the whole wave (three quarters of level 0's, tools'
                     // density model): every marked cell is free only -- updateSetFree alone
 #pragma unroll

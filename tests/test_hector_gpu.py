@@ -556,8 +556,8 @@ def test_batch_sizes_across_split_rules(gpu, B):
 
 @pytest.mark.parametrize("split", ["", "1,1,1", "6,3,2"])
 def test_ring_kernel_equals_clip_kernel(gpu, monkeypatch, split):
-    """The round-4 ring-ordered cursor update (default) and round 3's per-tile clipping kernel
-    (SLAM2D_UPD_KERNEL=clip) on the same 96-stream fleet, 4 steps, 2048^2 x 3 levels: every stream's pose and
+    """The round-4 ring-ordered cursor update (opt-in, SLAM2D_UPD_KERNEL=ring) and the per-tile clipping kernel
+    (default) on the same 96-stream fleet, 4 steps, 2048^2 x 3 levels: every stream's pose and
     every cell of sampled streams identical -- including ring-range parts (SLAM2D_UPD_SPLIT)."""
     import torch
 
@@ -567,8 +567,7 @@ def test_ring_kernel_equals_clip_kernel(gpu, monkeypatch, split):
         monkeypatch.setenv("SLAM2D_UPD_SPLIT", split)
     fleets = {}
     for kern in ("ring", "clip"):
-        if kern == "clip":
-            monkeypatch.setenv("SLAM2D_UPD_KERNEL", "clip")
+        monkeypatch.setenv("SLAM2D_UPD_KERNEL", kern)
         f = HectorFleet(B, 0.05, 2048, (0.5, 0.5), 3, max_points=1081)
         f.set_update_factors(0.4, 0.9)
         f.set_thresholds(-1.0, -1.0)

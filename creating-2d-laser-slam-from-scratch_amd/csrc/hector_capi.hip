@@ -126,6 +126,7 @@ struct hs_ctx {
     float *d_ranges1 = nullptr;
     // clock probe buffer (hs_set_clock_probe): 8 counters, see FleetGeom::clk
     unsigned long long *d_clk = nullptr;
+    size_t stream_pad_words = 0;  // see init_geometry
 };
 
 namespace {
@@ -170,7 +171,11 @@ void init_geometry(hs_ctx *c)
         ry /= 2;
         res *= 2.0f;
     }
-    g.stream_words = off;
+    // per-stream pad (SLAM2D_STREAM_PAD bytes, a multiple of 256): a stream's levels add up to a multiple of
+    // 2 MB, so without it the same tile of every stream sits at the same offset modulo every power-of-two
+    // interleave period of the memory system
+    g.stream_words = off + c->stream_pad_words;
+    g.cells_words = off;
 }
 
 // GridMapLogOddsFunctions::probToLogOdds  GridMapLogOdds.h:153-157
@@ -199,7 +204,8 @@ StreamState initial_state()
 int reset_all(hs_ctx *c, bool full)
 {
     size_t nwords = c->cells_bytes / sizeof(float);
-    hipLaunchKernelGGL(hs_fill_cells_kernel, dim3(4096), dim3(256), 0, c->stream, c->d_cells, nwords);
+    hipLaunchKernelGGL(hs_fill_cells_kernel, dim3(4096), dim3(256), 0, c->stream, c->d_cells, nwords,
+                       c->geom.stream_words);
     HCHK(hipGetLastError());
     std::vector<StreamState> h(c->B, initial_state());
     if (!full) {
@@ -509,6 +515,7 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
     c->res = map_resolution;
     c->start_x = map_start_x;
     c->start_y = map_start_y;
+    if (const char *sp = getenv("SLAM2D_STREAM_PAD")) c->stream_pad_words = (size_t)(atoll(sp) / 256) * 64;
     init_geometry(c);
     c->geom.lf = prob_to_logodds(0.4f);  // GridMapLogOddsFunctions ctor (GridMapLogOdds.h:98-102)
     c->geom.lo = prob_to_logodds(0.6f);

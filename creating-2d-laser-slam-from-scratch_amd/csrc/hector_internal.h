@@ -74,7 +74,8 @@ struct FleetGeom {
     int levels;
     float lf, lo;              // logOddsFree / logOddsOccupied
     float min_dist, min_ang;   // map update thresholds
-    size_t stream_words;       // 4-byte words per stream (all levels, tiled, both planes)
+    size_t stream_words;       // 4-byte words per stream (all levels, tiled, both planes; + the stream pad)
+    size_t cells_words;        // of which cells (the levels)
     int upd_parts[MAX_LEVELS]; // hs_update_kernel workgroups per (stream, level)
     int upd_minp[MAX_LEVELS];  // list-driven split: at least this many workgroups per level (0: upd_split's)
     // clock probe (hs_set_clock_probe; NULL = off): [kernel * 4 + {0: shader cycles, 1: 100-MHz ticks,

@@ -741,10 +741,11 @@ constexpr int CW_NP = 6;                           // slots per point thread
 constexpr int CW_MAXN = CW_PTS * CW_NP;            // 1152 points in registers
 constexpr int CW_STRIDE = CW_PTS + 4;              // term-buffer row (words): 16-B aligned, row k on bank 4k
 constexpr int CW_BUF = 9 * CW_STRIDE;              // one chunk's terms
-// term buffers: 2 (one barrier per chunk; 38.6 KB of LDS, 4 workgroups per CU) or 1 (two barriers per chunk;
-// 31.6 KB with REGS, 5 workgroups per CU)
+// term buffers: 1 (default: two barriers per chunk; 31.3 KB of LDS with REGS, 5 workgroups per CU) or 2 (one
+// barrier per chunk; 38.3 KB, 4 workgroups per CU).  Measured (profiles/r04/ab_r04d*): match 0.340 / 0.345 ms at
+// 2048 streams; at 2560 streams (two whole rounds at 5 per CU) the one-buffer match is 0.395 ms, 1.56 M scans/s
 #ifndef S2D_CW_BUFS
-#define S2D_CW_BUFS 2
+#define S2D_CW_BUFS 1
 #endif
 constexpr int CW_BUFS = S2D_CW_BUFS;
 #ifndef S2D_MATCH_CW
@@ -2825,14 +2826,24 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
 }
 
 // --------------------------------------------------------------------------- utility kernels
-__global__ void hs_fill_cells_kernel(float *__restrict__ words, size_t n)
+__global__ void hs_fill_cells_kernel(float *__restrict__ words, size_t n, size_t stream_words)
 {
-    // LogOddsCell::resetGridCell  H/map/GridMapLogOdds.h:76-80 : log-odds plane 0.0f, updateIndex plane -1
+    // LogOddsCell::resetGridCell  H/map/GridMapLogOdds.h:76-80 : log-odds plane 0.0f, updateIndex plane -1.
+    // The plane of a word follows from its offset inside its stream (levels start at multiples of a tile
+    // block; a per-stream pad, if any, is filled too and never read)
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t stream = i / stream_words, w = i - stream * stream_words;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t ds = stride / stream_words, dw = stride - ds * stream_words;
     for (; i < n; i += stride) {
-        if ((i / TILE_CELLS) & 1) reinterpret_cast<int *>(words)[i] = -1;
+        if ((w / TILE_CELLS) & 1) reinterpret_cast<int *>(words)[i] = -1;
         else words[i] = 0.0f;
+        w += dw;  // (stream, w) of i + stride without a division per word
+        stream += ds;
+        if (w >= stream_words) {
+            w -= stream_words;
+            ++stream;
+        }
     }
 }
 

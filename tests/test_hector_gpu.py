@@ -611,3 +611,36 @@ def test_clock_probe(gpu):
     for k in ("match", "update"):
         assert c[k]["workgroups_sampled"] > 0, c
         assert 300.0 < c[k]["sclk_mhz"] < 3000.0, c
+
+
+@pytest.mark.parametrize("pad", ["4352", "69888"])
+def test_stream_pad_layout(gpu, monkeypatch, pad):
+    """SLAM2D_STREAM_PAD staggers the streams' blocks in memory: reset fills the planes per stream, and 3
+    streams x 4 steps stay bit-exact vs the oracle (poses and both planes of every level)."""
+    import torch
+
+    monkeypatch.setenv("SLAM2D_STREAM_PAD", pad)
+    B, T = 3, 4
+    S = synth.make_streams(B, T, seed=17)
+    fleet = HectorFleet(B, 0.05, 512, (0.5, 0.5), 2, max_points=1081)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(-1.0, -1.0)
+    oras = [O.HectorOracle(0.05, 512, (0.5, 0.5), 2, reduce_threads=T_RED) for _ in range(B)]
+    for o in oras:
+        o.set_update_factors(0.4, 0.9)
+        o.set_thresholds(-1.0, -1.0)
+    for t in range(T):
+        d_xy = _torch_dev(S.points[:, t])
+        d_n = _torch_dev(S.counts[:, t].astype(np.int32))
+        fleet.step_device(d_xy.data_ptr(), 1081, d_n.data_ptr())
+        torch.cuda.synchronize()
+        gp = fleet.poses()[0]
+        for s in range(B):
+            op, _, _ = oras[s].process(S.points[s, t, : S.counts[s, t]])
+            np.testing.assert_array_equal(_bits(gp[s]), _bits(op), err_msg=f"t={t} s={s}")
+    for s in range(B):
+        for lvl in range(2):
+            m = fleet.get_map(s, lvl)
+            ol, ou = oras[s].level(lvl)
+            np.testing.assert_array_equal(m["upd"], ou)
+            np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol))

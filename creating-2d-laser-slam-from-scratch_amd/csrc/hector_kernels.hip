@@ -1818,6 +1818,39 @@ constexpr int UPD_QUADS = TILE * UPD_TH / 4 / UPD_THREADS;  // apply quads per t
 // bit 4 + c "odd event word", bit 8 + c "hit" for its cells c = 0..3.
 // GridMapLogOddsFunctions (GridMapLogOdds.h:108-129) applied to one marked cell:
 // bit k of m set ? a : b, as a bitwise select on the float bits (no compare, no exec-mask branch)
+// The apply's stores: plain, or non-temporal (S2D_NT_STORE=1: a written cell is next touched one scan later,
+// after ~3.5 GB of other traffic, so keeping its line in L2 / the Infinity Cache buys nothing)
+#ifndef S2D_NT_STORE
+#define S2D_NT_STORE 0
+#endif
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef int nt_i4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void upd_store(float4 *p, float4 v)
+{
+#if S2D_NT_STORE
+    const nt_f4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<nt_f4 *>(p));
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void upd_store(int4 *p, int4 v)
+{
+#if S2D_NT_STORE
+    const nt_i4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<nt_i4 *>(p));
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void upd_store(int *p, int v)
+{
+#if S2D_NT_STORE
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 __device__ __forceinline__ float bit_select(unsigned m, int k, float a, float b)
 {
     const int sel = ((int)(m << (31 - k))) >> 31;  // 0 or -1
@@ -2221,13 +2254,13 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 // log-odds: the whole quad was loaded, so it is stored whole (one instruction; unmarked
                 // cells rewrite their own value); updateIndex: whole when every cell is marked, else
                 // per marked cell (its unmarked cells were never read)
-                *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);
+                upd_store(reinterpret_cast<float4 *>(&pend_tl[o]), make_float4(nv[0], nv[1], nv[2], nv[3]));
                 if ((mb & 15u) == 15u) {
-                    *reinterpret_cast<int4 *>(&tu[o]) = make_int4(uv[0], uv[1], uv[2], uv[3]);
+                    upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));
                 } else {
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        if ((mb >> c) & 1u) tu[o + (unsigned)c] = uv[c];
+                        if ((mb >> c) & 1u) upd_store(&tu[o + (unsigned)c], uv[c]);
                 }
                 touched += __popc(mb & 15u);
             }

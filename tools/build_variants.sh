@@ -4,6 +4,7 @@
 #   cw2   chain-wave match with two term buffers (S2D_CW_BUFS=2: 38 KB of LDS, 4 workgroups per CU)
 #   r3m   round 3's match chain (S2D_MATCH_CW=0)
 #   noaf  no apply fast path (S2D_APPLY_FAST=0)
+#   nt    non-temporal stores in the update apply (S2D_NT_STORE=1)
 set -e
 cd "$(dirname "$0")/../creating-2d-laser-slam-from-scratch_amd/csrc"
 make -s
@@ -12,3 +13,4 @@ make -s OUT=../lib/libslam2d_cw2.so EXTRA=-DS2D_CW_BUFS=2
 make -s OUT=../lib/libslam2d_r3m.so EXTRA=-DS2D_MATCH_CW=0
 
 make -s OUT=../lib/libslam2d_noaf.so EXTRA=-DS2D_APPLY_FAST=0
+make -s OUT=../lib/libslam2d_nt.so EXTRA=-DS2D_NT_STORE=1

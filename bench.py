@@ -33,10 +33,10 @@ METRIC = "scans/sec (1081-beam) Hector match+grid-update @1 GPU; pose RMSE vs re
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 
 CONFIGS = {
-    # hector_slam.launch defaults (hector_slam.cc:138-142): 2048^2, 3 levels -- the north-star grid
-    # 2048 streams x 44 MB pyramids = 90 GB of HBM (round-2 sweep, same kernels: 1024 streams 1.17 M,
-    # 2048 1.35 M, 4096 1.39 M scans/s; 2048 is where the per-stream update time stops falling)
-    "northstar": dict(map_size=2048, levels=3, streams=2048),
+    # hector_slam.launch defaults (hector_slam.cc:138-142): 2048^2, 3 levels -- the north-star grid.
+    # 2560 streams x 42 MB pyramids = 108 GB of HBM: two whole rounds of the match at 5 workgroups per CU
+    # (round 4, one lease: 1.56 M scans/s vs 1.48 M at 2048 streams, profiles/r04/ab_r04d*.md)
+    "northstar": dict(map_size=2048, levels=3, streams=2560),
     # BASELINE configs[1]: single-res 1024^2
     "c2": dict(map_size=1024, levels=1, streams=1024),
     # BASELINE configs[2]: 3-level 4096^2

@@ -1792,6 +1792,13 @@ constexpr int UPD_STRIDE = S2D_UPD_STRIDE;
 #ifndef S2D_APPLY_FAST
 #define S2D_APPLY_FAST 1  // 0: every marked quad takes the full apply_cell sequence (A/B)
 #endif
+#ifndef S2D_OCTET
+// 1: a thread's two apply quads are the two rows of one 32-byte sector (x % 4 == 0, rows 2k and 2k + 1 of a
+// 4 x 4 block) and the log-odds of both are loaded and stored together whenever either has a mark, so every
+// log-odds store is a whole sector (A/B: partial-sector writes against the extra bytes); 2: the updateIndex
+// plane too (its sectors loaded as well)
+#define S2D_OCTET 0
+#endif
 #ifndef S2D_UPD_TH
 #define S2D_UPD_TH 32
 #endif
@@ -1875,6 +1882,20 @@ __device__ __forceinline__ int upd_off(int row, int c4, int tiles_x)
     if constexpr (UPD_TH == TILE_H) return tile_cell(c4, row);
     return (row / TILE_H) * tiles_x * TILE_BLOCK_WORDS + tile_cell(c4, row % TILE_H);
 }
+
+// apply quad j of thread tid: row and first column.  Default: quads q = tid + j * 256 (16 per 64-cell row);
+// S2D_OCTET: rows 2 (tid / 16) + j of column group tid % 16 -- one 32-byte sector of a 4 x 4 block
+__device__ __forceinline__ int apply_row(int tid, int j)
+{
+    if constexpr (S2D_OCTET) return ((tid >> 4) << 1) + j;
+    return (int)(((unsigned)tid + (unsigned)(j * 256)) >> 4);
+}
+__device__ __forceinline__ int apply_c4(int tid, int j)
+{
+    if constexpr (S2D_OCTET) return (tid & 15) << 2;
+    return (int)((((unsigned)tid + (unsigned)(j * 256)) & 15u) << 2);
+}
+static_assert(!S2D_OCTET || (UPD_QUADS == 2 && UPD_TH == TILE_H), "octet apply: two quads per thread, 32-row tiles");
 
 constexpr int UPD_HIT_WORDS = UPD_TH * (TILE / 32);                  // one hit bit per tile cell
 constexpr int UPD_MARK_WORDS = (UPD_TILE_WORDS + UPD_HIT_WORDS + 3) & ~3;
@@ -2069,6 +2090,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     // tile is now a ballot, and the extra state cost the kernel two spilled VGPRs.)
     float4 ql[UPD_QUADS];      // pending tile: log-odds of the marked quads (loads in flight)
     unsigned qb[UPD_QUADS];    // pending tile: 12 mark bits per quad (see apply_cell)
+    int4 qu[UPD_QUADS];        // S2D_OCTET == 2: pending tile's updateIndex of the marked sectors
     float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)
     // tile t = part + i * parts of the box (row-major): its column and row are carried from tile to tile
     // (a division of t by the box width per tile was ~20 scalar instructions of signed-division code)
@@ -2221,9 +2243,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
 #pragma unroll
             for (int j = 0; j < UPD_QUADS; ++j) {
                 const unsigned mb = qb[j];
-                if (!(mb & 15u)) continue;
-                const int qi = tid + j * UPD_THREADS;
-                const unsigned o = (unsigned)upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
+                if (!((S2D_OCTET ? qb[0] | qb[UPD_QUADS - 1] : mb) & 15u)) continue;
+                const unsigned o = (unsigned)upd_off(apply_row(tid, j), apply_c4(tid, j), g.tiles_x);
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
@@ -2255,7 +2276,14 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 // cells rewrite their own value); updateIndex: whole when every cell is marked, else
                 // per marked cell (its unmarked cells were never read)
                 upd_store(reinterpret_cast<float4 *>(&pend_tl[o]), make_float4(nv[0], nv[1], nv[2], nv[3]));
-                if ((mb & 15u) == 15u) {
+                if (S2D_OCTET == 2) {
+                    // whole sectors in the updateIndex plane too: the unmarked cells' indices were loaded
+                    const int ou[4] = {qu[j].x, qu[j].y, qu[j].z, qu[j].w};
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        uv[c] = __float_as_int(bit_select(mb, c, __int_as_float(uv[c]), __int_as_float(ou[c])));
+                    upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));
+                } else if ((mb & 15u) == 15u) {
                     upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));
                 } else {
 #pragma unroll
@@ -2274,8 +2302,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 pend_tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
 #pragma unroll
                 for (int j = 0; j < UPD_QUADS; ++j) {
-                    const unsigned qi = (unsigned)tid + j * UPD_THREADS;
-                    const int row = (int)(qi >> 4), c4 = (int)((qi & 15u) << 2);
+                    const int row = apply_row(tid, j), c4 = apply_c4(tid, j);
                     const int mw = lds_row(row) + c4;
                     const uint4 m = *reinterpret_cast<const uint4 *>(&marks[mw]);
                     const unsigned h = (hitb[row * (TILE / 32) + (c4 >> 5)] >> (c4 & 31)) & 15u;
@@ -2285,12 +2312,22 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     qb[j] = mk | ((od & mk) << 4) | ((h & mk) << 8);
                     // unsigned 32-bit offset: the load takes the scalar-base + VGPR-offset form, so nothing but
                     // the load itself writes its destination registers
-                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));
+                    if (!S2D_OCTET && mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));
                     // restore: the quad's event words (read by this thread only) and, by the first of
                     // the 8 lanes sharing it, the hit-bit word (its readers are this wave's lanes, whose
                     // read above precedes this write)
                     if (mk) *reinterpret_cast<uint4 *>(&marks[mw]) = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
                     if ((tid & 7) == 0) hitb[row * (TILE / 32) + (c4 >> 5)] = 0u;
+                }
+                if (S2D_OCTET && ((qb[0] | qb[UPD_QUADS - 1]) & 15u)) {
+                    // both rows of the sector (contiguous: the second row is the next 16 bytes of the block)
+                    const unsigned o = (unsigned)upd_off(apply_row(tid, 0), apply_c4(tid, 0), g.tiles_x);
+                    ql[0] = *reinterpret_cast<const float4 *>(pend_tl + o);
+                    ql[UPD_QUADS - 1] = *reinterpret_cast<const float4 *>(pend_tl + o + 4u);
+                    if (S2D_OCTET == 2) {
+                        qu[0] = *reinterpret_cast<const int4 *>(pend_tl + TILE_CELLS + o);
+                        qu[UPD_QUADS - 1] = *reinterpret_cast<const int4 *>(pend_tl + TILE_CELLS + o + 4u);
+                    }
                 }
             }
         }

@@ -5,6 +5,8 @@
 #   r3m   round 3's match chain (S2D_MATCH_CW=0)
 #   noaf  no apply fast path (S2D_APPLY_FAST=0)
 #   nt    non-temporal stores in the update apply (S2D_NT_STORE=1)
+#   oct   whole-sector log-odds stores in the update apply (S2D_OCTET=1)
+#   oct2  whole-sector stores in both planes (S2D_OCTET=2; 6 workgroups per CU for the extra registers)
 set -e
 cd "$(dirname "$0")/../creating-2d-laser-slam-from-scratch_amd/csrc"
 make -s
@@ -14,3 +16,5 @@ make -s OUT=../lib/libslam2d_r3m.so EXTRA=-DS2D_MATCH_CW=0
 
 make -s OUT=../lib/libslam2d_noaf.so EXTRA=-DS2D_APPLY_FAST=0
 make -s OUT=../lib/libslam2d_nt.so EXTRA=-DS2D_NT_STORE=1
+make -s OUT=../lib/libslam2d_oct.so EXTRA=-DS2D_OCTET=1
+make -s OUT=../lib/libslam2d_oct2.so EXTRA="-DS2D_OCTET=2 -DS2D_UPD_MINB=6"

@@ -1934,7 +1934,55 @@ __device__ __forceinline__ int fan_beam(int b0, int lane)  // b0 = 256 G + 64 w
 #endif
 }
 __host__ __device__ constexpr int fan_groups(int max_points) { return ((max_points + 255) / 256) * 4; }
-constexpr int UPD_GROUP_WORDS = 4;  // LDS words per fan group: its bounding box
+#ifndef S2D_WEDGE
+// 1: besides its bounding box, each fan group keeps the cone of its rays (the two extreme directions from the
+// scan origin, widened by two cells) and the per-tile cull drops the groups whose cone misses the tile -- for a
+// fan at an angle to the axes most of its box lies outside the cone, and there every lane whose ray's own box
+// meets the tile ran the whole clip setup to find no step inside it
+#define S2D_WEDGE 0
+#endif
+constexpr int UPD_GROUP_WORDS = S2D_WEDGE ? 8 : 4;  // LDS words per fan group: its bounding box (+ its cone)
+constexpr int UPD_GROUP_I4 = UPD_GROUP_WORDS / 4;
+
+// The cone of a fan group (S2D_WEDGE): the most counter-clockwise / clockwise ray directions (dx, dy) from
+// the origin cell among the wave's valid rays, {ccw.x, ccw.y, cw.x, cw.y}; all zero (no cone: the box alone
+// decides) when no ray is valid or a ray lies 90 degrees or more from the first valid one.  Every cell a ray
+// of the group marks lies within one cell of its ideal segment (the Bresenham minor coordinate is within
+// 1/2 + 1/(2 da) of the line), so a cell p (relative to the origin) is marked only if cross(cw, p) >= -|cw|
+// and cross(ccw, p) <= |ccw| -- tested with 2 max(|dx|, |dy|) >= |d| as the margin.
+__device__ __forceinline__ int4 fan_cone(bool valid, int dx, int dy)
+{
+    const unsigned long long vm = __ballot(valid);
+    if (!vm) return make_int4(0, 0, 0, 0);
+    const int rl = __builtin_ctzll(vm);
+    const int rdx = __shfl(dx, rl, 64), rdy = __shfl(dy, rl, 64);
+    // |components| <= 2^14 (upd_single_ok): exact 24-bit products
+    const int dot = __mul24(rdx, dx) + __mul24(rdy, dy);
+    const int crs = __mul24(rdx, dy) - __mul24(rdy, dx);
+    if (!__all((int)!valid | (int)(dot > 0))) return make_int4(0, 0, 0, 0);
+    // tangent of the angle from the reference ray (ordering only: a near tie picks a ray within ~1e-6 rad of
+    // the extreme, far inside the margin)
+    const float t = valid ? (float)crs * __builtin_amdgcn_rcpf((float)dot) : 0.0f;
+    float tmax = valid ? t : -3.0e38f, tmin = valid ? t : 3.0e38f;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        tmax = fmaxf(tmax, __shfl_xor(tmax, off, 64));
+        tmin = fminf(tmin, __shfl_xor(tmin, off, 64));
+    }
+    const int la = __builtin_ctzll(__ballot(valid && t == tmax));
+    const int lb = __builtin_ctzll(__ballot(valid && t == tmin));
+    return make_int4(__shfl(dx, la, 64), __shfl(dy, la, 64), __shfl(dx, lb, 64), __shfl(dy, lb, 64));
+}
+
+// may a fan group with cone w (fan_cone) mark a cell of the rectangle [px0, px1] x [py0, py1] (relative to
+// the origin cell)?  The extremes over the rectangle of the two linear cross products, against the margins.
+__device__ __forceinline__ bool cone_meets(const int4 w, int px0, int px1, int py0, int py1)
+{
+    const int cw_max = __mul24(w.z, w.z >= 0 ? py1 : py0) - __mul24(w.w, w.w >= 0 ? px0 : px1);
+    const int ccw_min = __mul24(w.x, w.x >= 0 ? py0 : py1) - __mul24(w.y, w.y >= 0 ? px1 : px0);
+    const int mcw = 2 * max(abs(w.z), abs(w.w)), mccw = 2 * max(abs(w.x), abs(w.y));
+    return (cw_max >= -mcw) & (ccw_min <= mccw);
+}
 
 // Grid: for level l, upd_parts[l] x count blocks (level-major, then part, then stream); part p of a
 // level draws the tiles t = p, p + parts, ... of the scan's tile box (t row-major over the box).
@@ -2040,7 +2088,12 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             gx1 = max(gx1, __shfl_xor(gx1, off, 64));
             gy1 = max(gy1, __shfl_xor(gy1, off, 64));
         }
-        if (lane == 0) gbox[b0 >> 6] = make_int4(gx0, gy0, gx1, gy1);
+        if (lane == 0) gbox[UPD_GROUP_I4 * (b0 >> 6)] = make_int4(gx0, gy0, gx1, gy1);
+        if constexpr (S2D_WEDGE) {
+            const bool vr = r != RAY_INVALID;
+            const int4 cone = fan_cone(vr, vr ? (int)(r & 0xFFFFu) - x0 : 0, vr ? (int)(r >> 16) - y0 : 0);
+            if (lane == 0) gbox[UPD_GROUP_I4 * (b0 >> 6) + 1] = cone;
+        }
     }
     if (R) {
         atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
@@ -2117,9 +2170,12 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             {
                 int ol = lane;  // opaque: the lane's box address is not hoisted into a VGPR held across tiles
                 asm volatile("" : "+v"(ol));
-                const int4 gb = gbox[min(ol, nfans - 1)];
-                fm = __ballot((int)(ol < nfans) & (int)(gb.z >= X0) & (int)(gb.x < X1) & (int)(gb.w >= Y0) &
-                              (int)(gb.y < Y1));
+                const int4 gb = gbox[UPD_GROUP_I4 * min(ol, nfans - 1)];
+                int in = (int)(ol < nfans) & (int)(gb.z >= X0) & (int)(gb.x < X1) & (int)(gb.w >= Y0) & (int)(gb.y < Y1);
+                if constexpr (S2D_WEDGE)
+                    in &= (int)cone_meets(gbox[UPD_GROUP_I4 * min(ol, nfans - 1) + 1], X0 - x0, X1 - 1 - x0, Y0 - y0,
+                                          Y1 - 1 - y0);
+                fm = __ballot(in);
             }
             {
                 // this wave's groups (fi = wave + 4 k) among the first 64 that meet the tile, one set bit each:
@@ -2135,7 +2191,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                         if ((b0x & ~255) >= n) break;
                         b0 = b0x;
                         b0x += UPD_THREADS;
-                        const int4 gb = gbox[b0 >> 6];
+                        const int4 gb = gbox[UPD_GROUP_I4 * (b0 >> 6)];
                         const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
                         const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
                         if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;

@@ -1934,6 +1934,12 @@ __device__ __forceinline__ int fan_beam(int b0, int lane)  // b0 = 256 G + 64 w
 #endif
 }
 __host__ __device__ constexpr int fan_groups(int max_points) { return ((max_points + 255) / 256) * 4; }
+#ifndef S2D_CULL_BATCH
+// 1: a wave culls its own fan groups for a batch of its next tiles at once -- lane j * G + k tests tile i + j
+// against the wave's group k (G slots per tile, a power of two >= its group count; 64 / G tiles per batch) --
+// and each tile takes its bits from that one ballot, instead of a ballot over every group per tile
+#define S2D_CULL_BATCH 0
+#endif
 #ifndef S2D_WEDGE
 // 1: besides its bounding box, each fan group keeps the cone of its rays (the two extreme directions from the
 // scan origin, widened by two cells) and the per-tile cull drops the groups whose cone misses the tile -- for a
@@ -2148,6 +2154,10 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     // tile t = part + i * parts of the box (row-major): its column and row are carried from tile to tile
     // (a division of t by the box width per tile was ~20 scalar instructions of signed-division code)
     int tcol = part % ntx, trow = part / ntx;
+    // S2D_CULL_BATCH: the wave's groups among the first 64 are f = wv + 4 k, k < kg; 2^gkl cull slots per tile
+    // (kg and the slot count recomputed where used: held across the tile loop they cost scalar spills)
+    const int gkl = nfans <= 4 ? 0 : 32 - __builtin_clz((unsigned)((min(nfans, 64) >> 2) - 1));
+    unsigned long long cullm = 0ull;
     for (int ii = 0; ii <= my_tiles; ++ii) {
         const int i = __builtin_amdgcn_readfirstlane(ii);  // uniform (the compiler had put it in a VGPR)
         const int ty = ty0 + trow, tx = tx0 + tcol;
@@ -2166,8 +2176,32 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             // the fan groups whose box meets the tile, one bit each: lane f tests group f, one ballot (the
             // scalar box test of every group of the wave on every tile cost ~20 SALU a time, most of them
             // on tiles no fan reaches); groups past the first 64 (scans of > 4096 points) test their box alone
-            unsigned long long fm;
-            {
+            unsigned long long fm = 0ull;
+            if constexpr (S2D_CULL_BATCH) {
+                if ((i & ((64 >> gkl) - 1)) == 0) {
+                    // opaque copies: everything below is recomputed per batch (hoisted out of the tile loop,
+                    // the lane masks, the reciprocal and the box address were spilled)
+                    int ol = lane, ontx = ntx;
+                    asm volatile("" : "+v"(ol));
+                    asm volatile("" : "+s"(ontx));
+                    const int j = ol >> gkl, k = ol & ((1 << gkl) - 1);
+                    const int ti = i + j;
+                    const int wv = wave_beam0 >> 6;
+                    int in = 0;
+                    if ((ti < my_tiles) & (k < (min(nfans, 64) >> 2))) {
+                        unsigned col;
+                        const unsigned row = udiv_small((unsigned)(part + ti * parts), (unsigned)ontx, col);
+                        const int X0j = (tx0 + (int)col) * TILE, Y0j = (ty0 + (int)row) * UPD_TH;
+                        const int f = wv + 4 * k;
+                        const int4 gb = gbox[UPD_GROUP_I4 * f];
+                        in = (int)(gb.z >= X0j) & (int)(gb.x < X0j + TILE) & (int)(gb.w >= Y0j) & (int)(gb.y < Y0j + UPD_TH);
+                        if constexpr (S2D_WEDGE)
+                            in &= (int)cone_meets(gbox[UPD_GROUP_I4 * f + 1], X0j - x0, X0j + TILE - 1 - x0, Y0j - y0,
+                                                  Y0j + UPD_TH - 1 - y0);
+                    }
+                    cullm = __ballot(in);
+                }
+            } else {
                 int ol = lane;  // opaque: the lane's box address is not hoisted into a VGPR held across tiles
                 asm volatile("" : "+v"(ol));
                 const int4 gb = gbox[UPD_GROUP_I4 * min(ol, nfans - 1)];
@@ -2180,12 +2214,14 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             {
                 // this wave's groups (fi = wave + 4 k) among the first 64 that meet the tile, one set bit each:
                 // the loop visits only those (scalar find-first-set), then the groups past 64 test their box
-                unsigned long long gm = fm & (0x1111111111111111ull << (wave_beam0 >> 6));
+                unsigned long long gm = S2D_CULL_BATCH ? (cullm >> ((i & ((64 >> gkl) - 1)) << gkl)) & ((2ull << ((1 << gkl) - 1)) - 1ull)
+                                                       : fm & (0x1111111111111111ull << (wave_beam0 >> 6));
                 int b0x = wave_beam0 + 64 * 64;  // groups >= 64 (scans of > 4096 points)
                 for (;;) {
                     int b0;
                     if (gm) {
-                        b0 = __builtin_ctzll(gm) << 6;
+                        // batch: bit k is group wv + 4 k (beams 256 k + 64 wv); else bit f is group f
+                        b0 = S2D_CULL_BATCH ? wave_beam0 + (__builtin_ctzll(gm) << 8) : __builtin_ctzll(gm) << 6;
                         gm &= gm - 1ull;
                     } else {
                         if ((b0x & ~255) >= n) break;

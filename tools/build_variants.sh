@@ -8,6 +8,7 @@
 #   oct   whole-sector log-odds stores in the update apply (S2D_OCTET=1)
 #   oct2  whole-sector stores in both planes (S2D_OCTET=2; 6 workgroups per CU for the extra registers)
 #   wedge fan groups culled per tile by the cone of their rays as well as their box (S2D_WEDGE=1)
+#   batch  fan-group cull batched over a wave's next tiles (S2D_CULL_BATCH=1); batchw: with the cone cull
 set -e
 cd "$(dirname "$0")/../creating-2d-laser-slam-from-scratch_amd/csrc"
 make -s
@@ -20,3 +21,5 @@ make -s OUT=../lib/libslam2d_nt.so EXTRA=-DS2D_NT_STORE=1
 make -s OUT=../lib/libslam2d_oct.so EXTRA=-DS2D_OCTET=1
 make -s OUT=../lib/libslam2d_oct2.so EXTRA="-DS2D_OCTET=2 -DS2D_UPD_MINB=6"
 make -s OUT=../lib/libslam2d_wedge.so EXTRA=-DS2D_WEDGE=1
+make -s OUT=../lib/libslam2d_batch.so EXTRA=-DS2D_CULL_BATCH=1
+make -s OUT=../lib/libslam2d_batchw.so EXTRA="-DS2D_CULL_BATCH=1 -DS2D_WEDGE=1"

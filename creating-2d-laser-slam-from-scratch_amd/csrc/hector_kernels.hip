@@ -1792,13 +1792,6 @@ constexpr int UPD_STRIDE = S2D_UPD_STRIDE;
 #ifndef S2D_APPLY_FAST
 #define S2D_APPLY_FAST 1  // 0: every marked quad takes the full apply_cell sequence (A/B)
 #endif
-#ifndef S2D_OCTET
-// 1: a thread's two apply quads are the two rows of one 32-byte sector (x % 4 == 0, rows 2k and 2k + 1 of a
-// 4 x 4 block) and the log-odds of both are loaded and stored together whenever either has a mark, so every
-// log-odds store is a whole sector (A/B: partial-sector writes against the extra bytes); 2: the updateIndex
-// plane too (its sectors loaded as well)
-#define S2D_OCTET 0
-#endif
 #ifndef S2D_UPD_TH
 #define S2D_UPD_TH 32
 #endif
@@ -1883,20 +1876,6 @@ __device__ __forceinline__ int upd_off(int row, int c4, int tiles_x)
     return (row / TILE_H) * tiles_x * TILE_BLOCK_WORDS + tile_cell(c4, row % TILE_H);
 }
 
-// apply quad j of thread tid: row and first column.  Default: quads q = tid + j * 256 (16 per 64-cell row);
-// S2D_OCTET: rows 2 (tid / 16) + j of column group tid % 16 -- one 32-byte sector of a 4 x 4 block
-__device__ __forceinline__ int apply_row(int tid, int j)
-{
-    if constexpr (S2D_OCTET) return ((tid >> 4) << 1) + j;
-    return (int)(((unsigned)tid + (unsigned)(j * 256)) >> 4);
-}
-__device__ __forceinline__ int apply_c4(int tid, int j)
-{
-    if constexpr (S2D_OCTET) return (tid & 15) << 2;
-    return (int)((((unsigned)tid + (unsigned)(j * 256)) & 15u) << 2);
-}
-static_assert(!S2D_OCTET || (UPD_QUADS == 2 && UPD_TH == TILE_H), "octet apply: two quads per thread, 32-row tiles");
-
 constexpr int UPD_HIT_WORDS = UPD_TH * (TILE / 32);                  // one hit bit per tile cell
 constexpr int UPD_MARK_WORDS = (UPD_TILE_WORDS + UPD_HIT_WORDS + 3) & ~3;
 
@@ -1934,61 +1913,7 @@ __device__ __forceinline__ int fan_beam(int b0, int lane)  // b0 = 256 G + 64 w
 #endif
 }
 __host__ __device__ constexpr int fan_groups(int max_points) { return ((max_points + 255) / 256) * 4; }
-#ifndef S2D_CULL_BATCH
-// 1: a wave culls its own fan groups for a batch of its next tiles at once -- lane j * G + k tests tile i + j
-// against the wave's group k (G slots per tile, a power of two >= its group count; 64 / G tiles per batch) --
-// and each tile takes its bits from that one ballot, instead of a ballot over every group per tile
-#define S2D_CULL_BATCH 0
-#endif
-#ifndef S2D_WEDGE
-// 1: besides its bounding box, each fan group keeps the cone of its rays (the two extreme directions from the
-// scan origin, widened by two cells) and the per-tile cull drops the groups whose cone misses the tile -- for a
-// fan at an angle to the axes most of its box lies outside the cone, and there every lane whose ray's own box
-// meets the tile ran the whole clip setup to find no step inside it
-#define S2D_WEDGE 0
-#endif
-constexpr int UPD_GROUP_WORDS = S2D_WEDGE ? 8 : 4;  // LDS words per fan group: its bounding box (+ its cone)
-constexpr int UPD_GROUP_I4 = UPD_GROUP_WORDS / 4;
-
-// The cone of a fan group (S2D_WEDGE): the most counter-clockwise / clockwise ray directions (dx, dy) from
-// the origin cell among the wave's valid rays, {ccw.x, ccw.y, cw.x, cw.y}; all zero (no cone: the box alone
-// decides) when no ray is valid or a ray lies 90 degrees or more from the first valid one.  Every cell a ray
-// of the group marks lies within one cell of its ideal segment (the Bresenham minor coordinate is within
-// 1/2 + 1/(2 da) of the line), so a cell p (relative to the origin) is marked only if cross(cw, p) >= -|cw|
-// and cross(ccw, p) <= |ccw| -- tested with 2 max(|dx|, |dy|) >= |d| as the margin.
-__device__ __forceinline__ int4 fan_cone(bool valid, int dx, int dy)
-{
-    const unsigned long long vm = __ballot(valid);
-    if (!vm) return make_int4(0, 0, 0, 0);
-    const int rl = __builtin_ctzll(vm);
-    const int rdx = __shfl(dx, rl, 64), rdy = __shfl(dy, rl, 64);
-    // |components| <= 2^14 (upd_single_ok): exact 24-bit products
-    const int dot = __mul24(rdx, dx) + __mul24(rdy, dy);
-    const int crs = __mul24(rdx, dy) - __mul24(rdy, dx);
-    if (!__all((int)!valid | (int)(dot > 0))) return make_int4(0, 0, 0, 0);
-    // tangent of the angle from the reference ray (ordering only: a near tie picks a ray within ~1e-6 rad of
-    // the extreme, far inside the margin)
-    const float t = valid ? (float)crs * __builtin_amdgcn_rcpf((float)dot) : 0.0f;
-    float tmax = valid ? t : -3.0e38f, tmin = valid ? t : 3.0e38f;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        tmax = fmaxf(tmax, __shfl_xor(tmax, off, 64));
-        tmin = fminf(tmin, __shfl_xor(tmin, off, 64));
-    }
-    const int la = __builtin_ctzll(__ballot(valid && t == tmax));
-    const int lb = __builtin_ctzll(__ballot(valid && t == tmin));
-    return make_int4(__shfl(dx, la, 64), __shfl(dy, la, 64), __shfl(dx, lb, 64), __shfl(dy, lb, 64));
-}
-
-// may a fan group with cone w (fan_cone) mark a cell of the rectangle [px0, px1] x [py0, py1] (relative to
-// the origin cell)?  The extremes over the rectangle of the two linear cross products, against the margins.
-__device__ __forceinline__ bool cone_meets(const int4 w, int px0, int px1, int py0, int py1)
-{
-    const int cw_max = __mul24(w.z, w.z >= 0 ? py1 : py0) - __mul24(w.w, w.w >= 0 ? px0 : px1);
-    const int ccw_min = __mul24(w.x, w.x >= 0 ? py0 : py1) - __mul24(w.y, w.y >= 0 ? px1 : px0);
-    const int mcw = 2 * max(abs(w.z), abs(w.w)), mccw = 2 * max(abs(w.x), abs(w.y));
-    return (cw_max >= -mcw) & (ccw_min <= mccw);
-}
+constexpr int UPD_GROUP_WORDS = 4;  // LDS words per fan group: its bounding box
 
 // Grid: for level l, upd_parts[l] x count blocks (level-major, then part, then stream); part p of a
 // level draws the tiles t = p, p + parts, ... of the scan's tile box (t row-major over the box).
@@ -2094,12 +2019,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             gx1 = max(gx1, __shfl_xor(gx1, off, 64));
             gy1 = max(gy1, __shfl_xor(gy1, off, 64));
         }
-        if (lane == 0) gbox[UPD_GROUP_I4 * (b0 >> 6)] = make_int4(gx0, gy0, gx1, gy1);
-        if constexpr (S2D_WEDGE) {
-            const bool vr = r != RAY_INVALID;
-            const int4 cone = fan_cone(vr, vr ? (int)(r & 0xFFFFu) - x0 : 0, vr ? (int)(r >> 16) - y0 : 0);
-            if (lane == 0) gbox[UPD_GROUP_I4 * (b0 >> 6) + 1] = cone;
-        }
+        if (lane == 0) gbox[b0 >> 6] = make_int4(gx0, gy0, gx1, gy1);
     }
     if (R) {
         atomicMin(&s_bbox[0], bx0); atomicMin(&s_bbox[1], by0);
@@ -2149,15 +2069,10 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     // tile is now a ballot, and the extra state cost the kernel two spilled VGPRs.)
     float4 ql[UPD_QUADS];      // pending tile: log-odds of the marked quads (loads in flight)
     unsigned qb[UPD_QUADS];    // pending tile: 12 mark bits per quad (see apply_cell)
-    int4 qu[UPD_QUADS];        // S2D_OCTET == 2: pending tile's updateIndex of the marked sectors
     float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)
     // tile t = part + i * parts of the box (row-major): its column and row are carried from tile to tile
     // (a division of t by the box width per tile was ~20 scalar instructions of signed-division code)
     int tcol = part % ntx, trow = part / ntx;
-    // S2D_CULL_BATCH: the wave's groups among the first 64 are f = wv + 4 k, k < kg; 2^gkl cull slots per tile
-    // (kg and the slot count recomputed where used: held across the tile loop they cost scalar spills)
-    const int gkl = nfans <= 4 ? 0 : 32 - __builtin_clz((unsigned)((min(nfans, 64) >> 2) - 1));
-    unsigned long long cullm = 0ull;
     for (int ii = 0; ii <= my_tiles; ++ii) {
         const int i = __builtin_amdgcn_readfirstlane(ii);  // uniform (the compiler had put it in a VGPR)
         const int ty = ty0 + trow, tx = tx0 + tcol;
@@ -2176,58 +2091,29 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             // the fan groups whose box meets the tile, one bit each: lane f tests group f, one ballot (the
             // scalar box test of every group of the wave on every tile cost ~20 SALU a time, most of them
             // on tiles no fan reaches); groups past the first 64 (scans of > 4096 points) test their box alone
-            unsigned long long fm = 0ull;
-            if constexpr (S2D_CULL_BATCH) {
-                if ((i & ((64 >> gkl) - 1)) == 0) {
-                    // opaque copies: everything below is recomputed per batch (hoisted out of the tile loop,
-                    // the lane masks, the reciprocal and the box address were spilled)
-                    int ol = lane, ontx = ntx;
-                    asm volatile("" : "+v"(ol));
-                    asm volatile("" : "+s"(ontx));
-                    const int j = ol >> gkl, k = ol & ((1 << gkl) - 1);
-                    const int ti = i + j;
-                    const int wv = wave_beam0 >> 6;
-                    int in = 0;
-                    if ((ti < my_tiles) & (k < (min(nfans, 64) >> 2))) {
-                        unsigned col;
-                        const unsigned row = udiv_small((unsigned)(part + ti * parts), (unsigned)ontx, col);
-                        const int X0j = (tx0 + (int)col) * TILE, Y0j = (ty0 + (int)row) * UPD_TH;
-                        const int f = wv + 4 * k;
-                        const int4 gb = gbox[UPD_GROUP_I4 * f];
-                        in = (int)(gb.z >= X0j) & (int)(gb.x < X0j + TILE) & (int)(gb.w >= Y0j) & (int)(gb.y < Y0j + UPD_TH);
-                        if constexpr (S2D_WEDGE)
-                            in &= (int)cone_meets(gbox[UPD_GROUP_I4 * f + 1], X0j - x0, X0j + TILE - 1 - x0, Y0j - y0,
-                                                  Y0j + UPD_TH - 1 - y0);
-                    }
-                    cullm = __ballot(in);
-                }
-            } else {
+            unsigned long long fm;
+            {
                 int ol = lane;  // opaque: the lane's box address is not hoisted into a VGPR held across tiles
                 asm volatile("" : "+v"(ol));
-                const int4 gb = gbox[UPD_GROUP_I4 * min(ol, nfans - 1)];
-                int in = (int)(ol < nfans) & (int)(gb.z >= X0) & (int)(gb.x < X1) & (int)(gb.w >= Y0) & (int)(gb.y < Y1);
-                if constexpr (S2D_WEDGE)
-                    in &= (int)cone_meets(gbox[UPD_GROUP_I4 * min(ol, nfans - 1) + 1], X0 - x0, X1 - 1 - x0, Y0 - y0,
-                                          Y1 - 1 - y0);
-                fm = __ballot(in);
+                const int4 gb = gbox[min(ol, nfans - 1)];
+                fm = __ballot((int)(ol < nfans) & (int)(gb.z >= X0) & (int)(gb.x < X1) & (int)(gb.w >= Y0) &
+                              (int)(gb.y < Y1));
             }
             {
                 // this wave's groups (fi = wave + 4 k) among the first 64 that meet the tile, one set bit each:
                 // the loop visits only those (scalar find-first-set), then the groups past 64 test their box
-                unsigned long long gm = S2D_CULL_BATCH ? (cullm >> ((i & ((64 >> gkl) - 1)) << gkl)) & ((2ull << ((1 << gkl) - 1)) - 1ull)
-                                                       : fm & (0x1111111111111111ull << (wave_beam0 >> 6));
+                unsigned long long gm = fm & (0x1111111111111111ull << (wave_beam0 >> 6));
                 int b0x = wave_beam0 + 64 * 64;  // groups >= 64 (scans of > 4096 points)
                 for (;;) {
                     int b0;
                     if (gm) {
-                        // batch: bit k is group wv + 4 k (beams 256 k + 64 wv); else bit f is group f
-                        b0 = S2D_CULL_BATCH ? wave_beam0 + (__builtin_ctzll(gm) << 8) : __builtin_ctzll(gm) << 6;
+                        b0 = __builtin_ctzll(gm) << 6;
                         gm &= gm - 1ull;
                     } else {
                         if ((b0x & ~255) >= n) break;
                         b0 = b0x;
                         b0x += UPD_THREADS;
-                        const int4 gb = gbox[UPD_GROUP_I4 * (b0 >> 6)];
+                        const int4 gb = gbox[b0 >> 6];
                         const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
                         const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
                         if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
@@ -2335,8 +2221,9 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
 #pragma unroll
             for (int j = 0; j < UPD_QUADS; ++j) {
                 const unsigned mb = qb[j];
-                if (!((S2D_OCTET ? qb[0] | qb[UPD_QUADS - 1] : mb) & 15u)) continue;
-                const unsigned o = (unsigned)upd_off(apply_row(tid, j), apply_c4(tid, j), g.tiles_x);
+                if (!(mb & 15u)) continue;
+                const int qi = tid + j * UPD_THREADS;
+                const unsigned o = (unsigned)upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
@@ -2368,14 +2255,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 // cells rewrite their own value); updateIndex: whole when every cell is marked, else
                 // per marked cell (its unmarked cells were never read)
                 upd_store(reinterpret_cast<float4 *>(&pend_tl[o]), make_float4(nv[0], nv[1], nv[2], nv[3]));
-                if (S2D_OCTET == 2) {
-                    // whole sectors in the updateIndex plane too: the unmarked cells' indices were loaded
-                    const int ou[4] = {qu[j].x, qu[j].y, qu[j].z, qu[j].w};
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-                        uv[c] = __float_as_int(bit_select(mb, c, __int_as_float(uv[c]), __int_as_float(ou[c])));
-                    upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));
-                } else if ((mb & 15u) == 15u) {
+                if ((mb & 15u) == 15u) {
                     upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));
                 } else {
 #pragma unroll
@@ -2394,7 +2274,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 pend_tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
 #pragma unroll
                 for (int j = 0; j < UPD_QUADS; ++j) {
-                    const int row = apply_row(tid, j), c4 = apply_c4(tid, j);
+                    const unsigned qi = (unsigned)tid + j * UPD_THREADS;
+                    const int row = (int)(qi >> 4), c4 = (int)((qi & 15u) << 2);
                     const int mw = lds_row(row) + c4;
                     const uint4 m = *reinterpret_cast<const uint4 *>(&marks[mw]);
                     const unsigned h = (hitb[row * (TILE / 32) + (c4 >> 5)] >> (c4 & 31)) & 15u;
@@ -2404,22 +2285,12 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     qb[j] = mk | ((od & mk) << 4) | ((h & mk) << 8);
                     // unsigned 32-bit offset: the load takes the scalar-base + VGPR-offset form, so nothing but
                     // the load itself writes its destination registers
-                    if (!S2D_OCTET && mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));
+                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));
                     // restore: the quad's event words (read by this thread only) and, by the first of
                     // the 8 lanes sharing it, the hit-bit word (its readers are this wave's lanes, whose
                     // read above precedes this write)
                     if (mk) *reinterpret_cast<uint4 *>(&marks[mw]) = make_uint4(W_NONE, W_NONE, W_NONE, W_NONE);
                     if ((tid & 7) == 0) hitb[row * (TILE / 32) + (c4 >> 5)] = 0u;
-                }
-                if (S2D_OCTET && ((qb[0] | qb[UPD_QUADS - 1]) & 15u)) {
-                    // both rows of the sector (contiguous: the second row is the next 16 bytes of the block)
-                    const unsigned o = (unsigned)upd_off(apply_row(tid, 0), apply_c4(tid, 0), g.tiles_x);
-                    ql[0] = *reinterpret_cast<const float4 *>(pend_tl + o);
-                    ql[UPD_QUADS - 1] = *reinterpret_cast<const float4 *>(pend_tl + o + 4u);
-                    if (S2D_OCTET == 2) {
-                        qu[0] = *reinterpret_cast<const int4 *>(pend_tl + TILE_CELLS + o);
-                        qu[UPD_QUADS - 1] = *reinterpret_cast<const int4 *>(pend_tl + TILE_CELLS + o + 4u);
-                    }
                 }
             }
         }

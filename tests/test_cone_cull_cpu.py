@@ -1,4 +1,6 @@
-"""CPU emulation of the update kernel's cone cull (S2D_WEDGE, hector_kernels.hip fan_cone / cone_meets).
+"""CPU emulation of the cone cull tried for the update kernel in round 4 (S2D_WEDGE: fan_cone / cone_meets in
+profiles/r04/update_variants_octet_wedge_batch.patch; measured slower, not in the product sources -- this pins the
+restatement tools/visit_model.py uses to count the clip setups it would remove).
 
 The cull may only drop a (tile, fan group) pair when no ray of the group marks a cell of the tile: every
 cell of the Bresenham walk of bresenham2D (lesson4/include/lesson4/hector_mapping/map/OccGridMapBase.h

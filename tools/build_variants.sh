@@ -5,10 +5,8 @@
 #   r3m   round 3's match chain (S2D_MATCH_CW=0)
 #   noaf  no apply fast path (S2D_APPLY_FAST=0)
 #   nt    non-temporal stores in the update apply (S2D_NT_STORE=1)
-#   oct   whole-sector log-odds stores in the update apply (S2D_OCTET=1)
-#   oct2  whole-sector stores in both planes (S2D_OCTET=2; 6 workgroups per CU for the extra registers)
-#   wedge fan groups culled per tile by the cone of their rays as well as their box (S2D_WEDGE=1)
-#   batch  fan-group cull batched over a wave's next tiles (S2D_CULL_BATCH=1); batchw: with the cone cull
+# (round 4's oct / oct2 / wedge / batch / batchw variants were measured slower or equal and removed from the
+# sources; their code is profiles/r04/update_variants_octet_wedge_batch.patch, results profiles/r04/ab_r04f.md, ab_r04g.md)
 set -e
 cd "$(dirname "$0")/../creating-2d-laser-slam-from-scratch_amd/csrc"
 make -s
@@ -18,8 +16,3 @@ make -s OUT=../lib/libslam2d_r3m.so EXTRA=-DS2D_MATCH_CW=0
 
 make -s OUT=../lib/libslam2d_noaf.so EXTRA=-DS2D_APPLY_FAST=0
 make -s OUT=../lib/libslam2d_nt.so EXTRA=-DS2D_NT_STORE=1
-make -s OUT=../lib/libslam2d_oct.so EXTRA=-DS2D_OCTET=1
-make -s OUT=../lib/libslam2d_oct2.so EXTRA="-DS2D_OCTET=2 -DS2D_UPD_MINB=6"
-make -s OUT=../lib/libslam2d_wedge.so EXTRA=-DS2D_WEDGE=1
-make -s OUT=../lib/libslam2d_batch.so EXTRA=-DS2D_CULL_BATCH=1
-make -s OUT=../lib/libslam2d_batchw.so EXTRA="-DS2D_CULL_BATCH=1 -DS2D_WEDGE=1"

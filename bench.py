@@ -34,9 +34,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 
 CONFIGS = {
     # hector_slam.launch defaults (hector_slam.cc:138-142): 2048^2, 3 levels -- the north-star grid.
-    # 2560 streams x 42 MB pyramids = 108 GB of HBM: two whole rounds of the match at 5 workgroups per CU
-    # (round 4, one lease: 1.56 M scans/s vs 1.48 M at 2048 streams, profiles/r04/ab_r04d*.md)
-    "northstar": dict(map_size=2048, levels=3, streams=2560),
+    # 3840 streams x 42 MB pyramids = 161 GB of HBM: three whole rounds of the match at 5 workgroups per CU
+    # (round 4, same lease: 1.58 M scans/s at 2560 streams, 1.64 M at 3840 -- the update's tail is a smaller
+    # share of a longer launch; 1.48 M at 2048: profiles/r04/ab_r04d*.md, ab_r04h_3840.md, r04h_summary.md)
+    "northstar": dict(map_size=2048, levels=3, streams=3840),
     # BASELINE configs[1]: single-res 1024^2
     "c2": dict(map_size=1024, levels=1, streams=1024),
     # BASELINE configs[2]: 3-level 4096^2

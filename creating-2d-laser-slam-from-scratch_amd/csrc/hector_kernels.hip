@@ -1856,6 +1856,58 @@ __device__ __forceinline__ float bit_select(unsigned m, int k, float a, float b)
     const int sel = ((int)(m << (31 - k))) >> 31;  // 0 or -1
     return __int_as_float((__float_as_int(a) & sel) | (__float_as_int(b) & ~sel));
 }
+
+// A quad's mark bits as hs_update_kernel carries them from the mark read to the apply.
+//   S2D_PACK_PERM 1 (default): the quad's four event words gathered by two byte permutes and one bit-field
+//   insert -- bit 7 + 8 c set when cell c is unmarked (the top bit of W_NONE; an event 2 b + {0, 1} is below
+//   2^31), bit QB_OD(c) the low bit of its event (odd: freed before its first hit), bit 1 + c its hit bit
+//   (rotated out of the row's hit word), all other bits don't-care: 6 VALU per quad instead of ~24 for
+//   the twelve compares / selects / shifts that built the compact nibbles.  A hit cell is always marked
+//   (its atomicMin of 2 b), so the hit and odd bits need no masking with the marks.
+//   0: the compact nibbles, bits c / 4 + c / 8 + c = marked / odd / hit (A/B).
+#ifndef S2D_PACK_PERM
+#define S2D_PACK_PERM 1
+#endif
+#if S2D_PACK_PERM
+__device__ __forceinline__ constexpr int qb_un(int c) { return 7 + 8 * c; }
+__device__ __forceinline__ constexpr int qb_od(int c) { return c < 2 ? 16 + 8 * c : 8 * (c - 2); }
+__device__ __forceinline__ constexpr int qb_hit(int c) { return 1 + c; }
+constexpr unsigned QB_UNMASK = 0x80808080u, QB_HITMASK = 0x1Eu;
+__device__ __forceinline__ unsigned qb_pack(uint4 m, unsigned hitw, int s)  // s: the quad's bit in hitw
+{
+    // P: bytes x.b3 y.b3 x.b0 y.b0 (unmarked x 7, y 15; odd x 16, y 24); Q: z.b0 w.b0 z.b3 w.b3 (odd z 0, w 8;
+    // unmarked z 23, w 31)
+    const unsigned P = __builtin_amdgcn_perm(m.y, m.x, 0x04000703u);
+    const unsigned Q = __builtin_amdgcn_perm(m.w, m.z, 0x07030400u);
+    const unsigned R = (P & 0x01018080u) | (Q & ~0x01018080u);
+    const unsigned h = __builtin_amdgcn_alignbit(hitw, hitw, (unsigned)(s - 1) & 31u);  // bits s..s+3 -> 1..4
+    return (h & QB_HITMASK) | (R & ~QB_HITMASK);
+}
+__device__ __forceinline__ bool qb_any(unsigned mb) { return (mb & QB_UNMASK) != QB_UNMASK; }
+__device__ __forceinline__ bool qb_all(unsigned mb) { return (mb & QB_UNMASK) == 0u; }
+__device__ __forceinline__ unsigned qb_count(unsigned mb) { return __popc(~mb & QB_UNMASK); }
+__device__ __forceinline__ bool qb_cell(unsigned mb, int c) { return !((mb >> qb_un(c)) & 1u); }
+__device__ __forceinline__ unsigned qb_hits(unsigned mb) { return mb & QB_HITMASK; }
+__device__ __forceinline__ float qb_sel_marked(unsigned mb, int c, float a, float b) { return bit_select(mb, qb_un(c), b, a); }
+#else
+__device__ __forceinline__ constexpr int qb_od(int c) { return 4 + c; }
+__device__ __forceinline__ constexpr int qb_hit(int c) { return 8 + c; }
+__device__ __forceinline__ unsigned qb_pack(uint4 m, unsigned hitw, int s)
+{
+    const unsigned h = (hitw >> s) & 15u;
+    const unsigned mk = (unsigned)(m.x != W_NONE) | ((unsigned)(m.y != W_NONE) << 1) | ((unsigned)(m.z != W_NONE) << 2) |
+                        ((unsigned)(m.w != W_NONE) << 3);
+    const unsigned od = (m.x & 1u) | ((m.y & 1u) << 1) | ((m.z & 1u) << 2) | ((m.w & 1u) << 3);
+    return mk | ((od & mk) << 4) | ((h & mk) << 8);
+}
+__device__ __forceinline__ bool qb_any(unsigned mb) { return (mb & 15u) != 0u; }
+__device__ __forceinline__ bool qb_all(unsigned mb) { return (mb & 15u) == 15u; }
+__device__ __forceinline__ unsigned qb_count(unsigned mb) { return __popc(mb & 15u); }
+__device__ __forceinline__ bool qb_cell(unsigned mb, int c) { return (mb >> c) & 1u; }
+__device__ __forceinline__ unsigned qb_hits(unsigned mb) { return (mb >> 8) & 15u; }
+__device__ __forceinline__ float qb_sel_marked(unsigned mb, int c, float a, float b) { return bit_select(mb, c, a, b); }
+#endif
+
 __device__ __forceinline__ float apply_cell(float l, unsigned odd, unsigned hit, float lf, float lo)
 {
     if (!hit) return l + lf;   // updateSetFree (:120-124)
@@ -2221,19 +2273,19 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
 #pragma unroll
             for (int j = 0; j < UPD_QUADS; ++j) {
                 const unsigned mb = qb[j];
-                if (!(mb & 15u)) continue;
+                if (!qb_any(mb)) continue;
                 const int qi = tid + j * UPD_THREADS;
                 const unsigned o = (unsigned)upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
                 int uv[4];
-                if (S2D_APPLY_FAST && !__any((mb >> 8) & 15u)) {
+                if (S2D_APPLY_FAST && !__any(qb_hits(mb))) {
                     // no end cell in this quad slot of the whole wave (about three quarters of level 0's on the
                     // synthetic scans): every marked cell is free only -- updateSetFree alone, two VALU per cell
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-                        nv[c] = bit_select(mb, c, lv[c] + lf, lv[c]);
+                        nv[c] = qb_sel_marked(mb, c, lv[c] + lf, lv[c]);
                         uv[c] = mark_free;
                     }
                 } else {
@@ -2245,24 +2297,24 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                         const float l = lv[c];
                         const float t = l + lf;                       // updateSetFree
                         const float u = t - lf;                       // ... then updateUnsetFree
-                        const float h = bit_select(mb, 4 + c, u, l);  // an earlier beam freed the hit cell
-                        const float oc = h < 50.0f ? h + lo : h;      // updateSetOccupied
-                        nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);
-                        uv[c] = __float_as_int(bit_select(mb, 8 + c, __int_as_float(mark_occ), __int_as_float(mark_free)));
+                        const float h = bit_select(mb, qb_od(c), u, l);  // an earlier beam freed the hit cell
+                        const float oc = h < 50.0f ? h + lo : h;         // updateSetOccupied
+                        nv[c] = qb_sel_marked(mb, c, bit_select(mb, qb_hit(c), oc, t), l);
+                        uv[c] = __float_as_int(bit_select(mb, qb_hit(c), __int_as_float(mark_occ), __int_as_float(mark_free)));
                     }
                 }
                 // log-odds: the whole quad was loaded, so it is stored whole (one instruction; unmarked
                 // cells rewrite their own value); updateIndex: whole when every cell is marked, else
                 // per marked cell (its unmarked cells were never read)
                 upd_store(reinterpret_cast<float4 *>(&pend_tl[o]), make_float4(nv[0], nv[1], nv[2], nv[3]));
-                if ((mb & 15u) == 15u) {
+                if (qb_all(mb)) {
                     upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));
                 } else {
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        if ((mb >> c) & 1u) upd_store(&tu[o + (unsigned)c], uv[c]);
+                        if (qb_cell(mb, c)) upd_store(&tu[o + (unsigned)c], uv[c]);
                 }
-                touched += __popc(mb & 15u);
+                touched += qb_count(mb);
             }
             pend_tl = nullptr;
         }
@@ -2278,11 +2330,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     const int row = (int)(qi >> 4), c4 = (int)((qi & 15u) << 2);
                     const int mw = lds_row(row) + c4;
                     const uint4 m = *reinterpret_cast<const uint4 *>(&marks[mw]);
-                    const unsigned h = (hitb[row * (TILE / 32) + (c4 >> 5)] >> (c4 & 31)) & 15u;
-                    const unsigned mk = (unsigned)(m.x != W_NONE) | ((unsigned)(m.y != W_NONE) << 1) |
-                                        ((unsigned)(m.z != W_NONE) << 2) | ((unsigned)(m.w != W_NONE) << 3);
-                    const unsigned od = (m.x & 1u) | ((m.y & 1u) << 1) | ((m.z & 1u) << 2) | ((m.w & 1u) << 3);
-                    qb[j] = mk | ((od & mk) << 4) | ((h & mk) << 8);
+                    qb[j] = qb_pack(m, hitb[row * (TILE / 32) + (c4 >> 5)], c4 & 31);
+                    const bool mk = qb_any(qb[j]);
                     // unsigned 32-bit offset: the load takes the scalar-base + VGPR-offset form, so nothing but
                     // the load itself writes its destination registers
                     if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));

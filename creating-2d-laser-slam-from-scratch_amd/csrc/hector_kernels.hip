@@ -160,12 +160,10 @@ struct MatchIngest {       // the fused ingest's buffers (ranges == nullptr: poi
 };
 
 // one beam of projectLaser + rosPointCloudToDataContainer: true if it becomes a DataContainer point
-__device__ __forceinline__ bool ingest_beam(const IngestGeom &ig, const double2 *__restrict__ cs, float range, int i,
-                                            float2 &p)
+__device__ __forceinline__ bool ingest_beam(const IngestGeom &ig, double2 u, float range, float2 &p)  // u = cs[beam]
 {
     bool keep = false;
     if (((double)range < ig.cutoff) && (range >= ig.range_min)) {  // projectLaser_
-        const double2 u = cs[i];
         const float x = (float)((double)range * u.x);
         const float y = (float)((double)range * u.y);
         const float z = 0.0f;
@@ -190,17 +188,66 @@ __device__ __forceinline__ bool ingest_beam(const IngestGeom &ig, const double2 
 }
 
 // the whole scan of one stream by a 256-thread workgroup: surviving points in beam order to out (and to
-// stage, an LDS copy, when given); returns the count (uniform).  s_w: 4 ints of LDS.
+// stage, an LDS copy, when given); returns the count (uniform).  s_w: ING_SW ints of LDS.
+// Scans of up to ING_CHUNKS x 256 beams: every range and unit vector is loaded up front (one memory latency
+// instead of one per 256-beam chunk) and the compaction takes ONE barrier (each wave's count per chunk, then
+// every thread's offset = the counts of the earlier chunks and of the lower waves of its own); longer scans
+// take the chunk loop (two barriers per chunk).
+constexpr int ING_CHUNKS = 5;  // 1280 beams
+#ifndef S2D_ING_PRELOAD
+#define S2D_ING_PRELOAD 1  // 0: the chunk loop for every scan (A/B)
+#endif
+constexpr int ING_SW = 4 * ING_CHUNKS;
 __device__ __forceinline__ int ingest_scan(const IngestGeom &ig, const double2 *__restrict__ cs,
                                            const float *__restrict__ r, float2 *__restrict__ out, float2 *stage,
                                            int *s_w)
 {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (S2D_ING_PRELOAD && ig.n <= 256 * ING_CHUNKS) {
+        float rr[ING_CHUNKS];
+        double2 uu[ING_CHUNKS];
+#pragma unroll
+        for (int c = 0; c < ING_CHUNKS; ++c) {
+            const int i = c * 256 + tid;
+            rr[c] = 0.0f;
+            uu[c] = make_double2(0.0, 0.0);
+            if (i < ig.n) {
+                rr[c] = r[i];
+                uu[c] = cs[i];
+            }
+        }
+        float2 pp[ING_CHUNKS];
+        unsigned keepm = 0u;  // bit c: this thread's beam of chunk c survives
+#pragma unroll
+        for (int c = 0; c < ING_CHUNKS; ++c) {
+            pp[c] = make_float2(0.0f, 0.0f);
+            const bool keep = c * 256 + tid < ig.n && ingest_beam(ig, uu[c], rr[c], pp[c]);
+            const unsigned long long m = __ballot(keep);
+            if (lane == 0) s_w[c * 4 + wv] = __popcll(m);
+            keepm |= keep ? 1u << c : 0u;
+        }
+        __syncthreads();
+        int base = 0;
+#pragma unroll
+        for (int c = 0; c < ING_CHUNKS; ++c) {
+            const int c0 = s_w[c * 4], c1 = s_w[c * 4 + 1], c2 = s_w[c * 4 + 2], c3 = s_w[c * 4 + 3];
+            const unsigned long long m = __ballot((keepm >> c) & 1u);
+            if ((keepm >> c) & 1u) {
+                const int off = base + (wv > 0 ? c0 : 0) + (wv > 1 ? c1 : 0) + (wv > 2 ? c2 : 0);
+                const int k = off + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                out[k] = pp[c];
+                if (stage) stage[k] = pp[c];
+            }
+            base += c0 + c1 + c2 + c3;
+        }
+        __syncthreads();  // s_w read by every thread before a caller reuses it
+        return base;
+    }
     int base = 0;
     for (int b0 = 0; b0 < ig.n; b0 += 256) {
         const int i = b0 + tid;
         float2 p = make_float2(0.0f, 0.0f);
-        const bool keep = i < ig.n && ingest_beam(ig, cs, r[i], i, p);
+        const bool keep = i < ig.n && ingest_beam(ig, cs[i], r[i], p);
         const unsigned long long m = __ballot(keep);
         if (lane == 0) s_w[wv] = __popcll(m);
         __syncthreads();
@@ -221,7 +268,7 @@ __global__ void __launch_bounds__(256)
 hs_ingest_kernel(IngestGeom ig, const double2 *__restrict__ cs, const float *__restrict__ ranges, int rstride,
                  float2 *__restrict__ xy, int xy_stride, int *__restrict__ n_out, float2 *__restrict__ origo_out)
 {
-    __shared__ int s_w[4];
+    __shared__ int s_w[ING_SW];
     const int s = blockIdx.x;
     const int n = ingest_scan(ig, cs, ranges + (size_t)s * rstride, xy + (size_t)s * xy_stride, nullptr, s_w);
     if (threadIdx.x == 0) {
@@ -955,7 +1002,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     load_exptab();
     __syncthreads();
     const float *scells = cells + (size_t)s * geom.stream_words;
-    __shared__ int s_w[4];
+    __shared__ int s_w[ING_SW];
     // fused ingest (mi.ranges): the scan's points in beam order to mi.xy_out (for the grid update) and to
     // an LDS copy in nb_val's space, read into registers below before nb_val's first use
     float2 *stage = reinterpret_cast<float2 *>(nb_val);

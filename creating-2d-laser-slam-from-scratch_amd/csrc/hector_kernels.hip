@@ -798,6 +798,13 @@ constexpr int CW_BUFS = S2D_CW_BUFS;
 #ifndef S2D_MATCH_CW
 #define S2D_MATCH_CW 1  // 0: round 3's chain wave that also computes terms (A/B builds)
 #endif
+// 1 (default; one term buffer only): the moved points' probability conversions are shared by all four waves --
+// the idle chain wave too -- over the three point waves' miss lists, between two barriers, instead of each point
+// wave converting its own list (the longest list set the start of chunk 0).  0: per-wave lists (A/B).
+#ifndef S2D_CW_SHARECONV
+#define S2D_CW_SHARECONV 1
+#endif
+constexpr bool CW_SHARE = S2D_CW_SHARECONV && CW_BUFS == 1;
 
 template <int NP>
 __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
@@ -809,6 +816,8 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
     const int wave = tid >> 6;
     const int nch = (n + CW_PTS - 1) / CW_PTS;  // chunks (uniform)
     float run = 0.0f;                           // chain wave, lane k < 9: the running sum of term k
+    __shared__ int s_mcnt[4];                   // CW_SHARE: each point wave's miss count
+    unsigned short *wl0 = reinterpret_cast<unsigned short *>(seqT + (CW_BUFS - 1) * CW_BUF);  // the miss lists
     if (wave != cw) {
         // the gathered log-odds of the moved points (the transform is recomputed for the terms below: keeping
         // px, py, fx, fy of every slot across the chunk loop cost more registers than 4 VALU per point)
@@ -866,13 +875,32 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
             }
             nmiss += __popcll(bm);
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (int e = lane; e < nmiss; e += 64) {
-            const int slot = wl[e];
+        if constexpr (CW_SHARE) {
+            if (lane == 0) s_mcnt[pw] = nmiss;
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            for (int e = lane; e < nmiss; e += 64) {
+                const int slot = wl[e];
+                const float4 v = nb_val[slot];
+                nb_val[slot] = make_float4(cell_prob(v.x), cell_prob(v.y), cell_prob(v.z), cell_prob(v.w));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+    }
+    if constexpr (CW_SHARE) {
+        // every wave converts entries wave * 64 + lane + 256 k of the three lists laid end to end; the second
+        // barrier also retires the lists before chunk 0's terms overwrite them
+        lds_barrier();
+        const int c0 = s_mcnt[0], c1 = s_mcnt[1], tot = c0 + c1 + s_mcnt[2];
+        for (int e = tid; e < tot; e += MATCH_THREADS) {
+            const int l = e < c0 ? 0 : (e < c0 + c1 ? 1 : 2);
+            const int slot = wl0[l * (NP * 64) + e - (l == 0 ? 0 : (l == 1 ? c0 : c0 + c1))];
             const float4 v = nb_val[slot];
             nb_val[slot] = make_float4(cell_prob(v.x), cell_prob(v.y), cell_prob(v.z), cell_prob(v.w));
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        lds_barrier();
+    }
+    if (wave != cw) {
         // chunk j = slot j of every point thread, in point order; buffer j & 1
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
@@ -897,7 +925,7 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
             }
             // (barriers only in wave-uniform control flow: a wave whose lanes straddle n runs both sides of
             // the slot test)
-            if (CW_BUFS == 1) lds_barrier();  // the chain wave is done with chunk j - 1 (j = 0: the miss lists)
+            if (CW_BUFS == 1 && (!CW_SHARE || j > 0)) lds_barrier();  // the chain wave is done with chunk j - 1 (j = 0: the miss lists)
             if (slot < n) {
                 float *T = seqT + (CW_BUFS == 2 ? (j & 1) * CW_BUF : 0);
 #pragma unroll
@@ -910,7 +938,7 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
         // (the workgroup's critical path issues ahead of co-resident workgroups' waves)
         __builtin_amdgcn_s_setprio(3);
         for (int j = 0; j < nch; ++j) {
-            if (CW_BUFS == 1) lds_barrier();
+            if (CW_BUFS == 1 && (!CW_SHARE || j > 0)) lds_barrier();
             lds_barrier();
             if (lane < 9)
                 run = seq_chain_t<CW_STRIDE>(seqT + (CW_BUFS == 2 ? (j & 1) * CW_BUF : 0), lane, min(CW_PTS, n - j * CW_PTS),

@@ -7,6 +7,7 @@
 #   nt    non-temporal stores in the update apply (S2D_NT_STORE=1)
 #   pk0   round-3 compact-nibble packing of the update's mark bits (S2D_PACK_PERM=0)
 #   ing0  ingest chunk loop for every scan (S2D_ING_PRELOAD=0)
+#   sc0   per-wave miss conversion in the chain-wave match (S2D_CW_SHARECONV=0)
 # (round 4's oct / oct2 / wedge / batch / batchw variants were measured slower or equal and removed from the
 # sources; their code is profiles/r04/update_variants_octet_wedge_batch.patch, results profiles/r04/ab_r04f.md, ab_r04g.md)
 set -e
@@ -20,3 +21,4 @@ make -s OUT=../lib/libslam2d_noaf.so EXTRA=-DS2D_APPLY_FAST=0
 make -s OUT=../lib/libslam2d_nt.so EXTRA=-DS2D_NT_STORE=1
 make -s OUT=../lib/libslam2d_pk0.so EXTRA=-DS2D_PACK_PERM=0
 make -s OUT=../lib/libslam2d_ing0.so EXTRA=-DS2D_ING_PRELOAD=0
+make -s OUT=../lib/libslam2d_sc0.so EXTRA=-DS2D_CW_SHARECONV=0

@@ -1027,14 +1027,14 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     const int s = stream_begin + local;
     StreamState &st = state[s];
     clk_stamp(geom.clk, 0, true);
-    load_exptab();
-    __syncthreads();
-    const float *scells = cells + (size_t)s * geom.stream_words;
-    __shared__ int s_w[ING_SW];
     // fused ingest (mi.ranges): the scan's points in beam order to mi.xy_out (for the grid update) and to
     // an LDS copy in nb_val's space, read into registers below before nb_val's first use
-    float2 *stage = reinterpret_cast<float2 *>(nb_val);
     const bool fused = mi.ranges != nullptr;
+    load_exptab();
+    if (!fused) __syncthreads();  // (fused: the ingest's barriers order the table before its first use)
+    const float *scells = cells + (size_t)s * geom.stream_words;
+    __shared__ int s_w[ING_SW];
+    float2 *stage = reinterpret_cast<float2 *>(nb_val);
     const float2 *pts = fused ? mi.xy_out + (size_t)local * xy_stride : xy + (size_t)local * xy_stride;
     const int n = fused ? ingest_scan(ig, mi.cs, mi.ranges + (size_t)local * mi.rstride,
                                       mi.xy_out + (size_t)local * xy_stride, stage, s_w)
@@ -1052,9 +1052,11 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     }
 
     float np_[3] = {hint[0], hint[1], hint[2]};
+    // the covariance: the last level's H after a match, else the stream's stored one (read only then, in the
+    // epilogue -- held from here it kept nine registers live through the whole match)
     float cov[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) cov[k] = st.cov[k];
+    bool cov_h = false;
+
     int clamps = 0;
     int parity = 0;
     if (mode == MODE_PROCESS || mode == MODE_MATCH_ONLY) {
@@ -1122,6 +1124,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             est[2] = normalize_angle(est[2]);
 #pragma unroll
             for (int k = 0; k < 9; ++k) cov[k] = H[k];
+            cov_h = true;
             world_from_map(g, est, tmp);
         }
         np_[0] = tmp[0];
@@ -1136,6 +1139,10 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
         wq->whole_used = 0;
     }
 
+    if (!cov_h) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) cov[k] = st.cov[k];
+    }
     if (out_pose) {
         out_pose[3 * local] = np_[0];
         out_pose[3 * local + 1] = np_[1];

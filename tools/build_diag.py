@@ -75,11 +75,11 @@ PATCHES = {
                    "    if (nw > 0) return true;\n    for (int t0 = lane; t0 < nw; t0 += 64 * 8) {\n        unsigned long long want[8], old[8];")],
     "ktstore": [("karto_kernels.hip", "                old[u] = atomicCAS(gw + wbase + r * wsw + q, 0ull, want[u]);",
                  "                gw[wbase + r * wsw + q] = want[u];")],
-    "phase1": [(K, "    load_exptab();\n    __syncthreads();\n    const float *scells",
-                "    if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_sleep(127);\n    load_exptab();\n    __syncthreads();\n    const float *scells")],
-    "phase2": [(K, "    load_exptab();\n    __syncthreads();\n    const float *scells",
+    "phase1": [(K, "    load_exptab();\n    if (!fused) __syncthreads();",
+                "    if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_sleep(127);\n    load_exptab();\n    if (!fused) __syncthreads();")],
+    "phase2": [(K, "    load_exptab();\n    if (!fused) __syncthreads();",
                 "    if ((blockIdx.x >> 8) & 1) { __builtin_amdgcn_s_sleep(127); __builtin_amdgcn_s_sleep(127); }\n"
-                "    load_exptab();\n    __syncthreads();\n    const float *scells")],
+                "    load_exptab();\n    if (!fused) __syncthreads();")],
     "noorigin": [(K, "                    if ((int)!met | (int)(lo_i > hi_i)) continue;\n",
                   "                    if (lo_i < 8) lo_i = 8;\n                    if (!met | (lo_i > hi_i)) continue;\n")],
     "nohitbit": [(K, "                    atomicOr(&hitb[c >> 5], 1u << (c & 31));\n", "                    (void)c;\n")],

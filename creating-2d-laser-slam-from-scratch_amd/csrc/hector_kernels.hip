@@ -805,6 +805,12 @@ constexpr int CW_BUFS = S2D_CW_BUFS;
 #define S2D_CW_SHARECONV 1
 #endif
 constexpr bool CW_SHARE = S2D_CW_SHARECONV && CW_BUFS == 1;
+// wave priority of every wave from a Gauss-Newton step's start to chunk 0's store (the phase the chain waits
+// for: transform, gathers, conversions, chunk 0's terms), so it issues ahead of co-resident workgroups' point
+// waves working ahead on later chunks; 0 = default priority (A/B)
+#ifndef S2D_PRECHAIN_PRIO
+#define S2D_PRECHAIN_PRIO 2
+#endif
 
 template <int NP>
 __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
@@ -818,6 +824,7 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
     float run = 0.0f;                           // chain wave, lane k < 9: the running sum of term k
     __shared__ int s_mcnt[4];                   // CW_SHARE: each point wave's miss count
     unsigned short *wl0 = reinterpret_cast<unsigned short *>(seqT + (CW_BUFS - 1) * CW_BUF);  // the miss lists
+    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);
     if (wave != cw) {
         // the gathered log-odds of the moved points (the transform is recomputed for the terms below: keeping
         // px, py, fx, fy of every slot across the chunk loop cost more registers than 4 VALU per point)
@@ -932,6 +939,7 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
                 for (int k = 0; k < 9; ++k) T[k * CW_STRIDE + pt] = t[k];
             }
             lds_barrier();  // chunk j stored (two buffers: and the chain wave is done with chunk j - 1)
+            if (S2D_PRECHAIN_PRIO && j == 0) __builtin_amdgcn_s_setprio(0);
         }
     } else {
         // the chain: lane k < 9 extends the sum of term k over each chunk, at s_setprio 3 through the step tail
@@ -1871,6 +1879,9 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
 // no stride changes -- tools/lds_sim.py: 2 % fewer raster LDS cycles -- and the unaligned quads cost the
 // apply more: measured 0.005 ms slower.)
 constexpr int UPD_STRIDE = S2D_UPD_STRIDE;
+#ifndef S2D_UPD_PRIO
+#define S2D_UPD_PRIO 0  // 1: hs_update_kernel raises a wave's priority by its share of the tile's fan groups (A/B)
+#endif
 #ifndef S2D_APPLY_FAST
 #define S2D_APPLY_FAST 1  // 0: every marked quad takes the full apply_cell sequence (A/B)
 #endif
@@ -2238,6 +2249,14 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 // the loop visits only those (scalar find-first-set), then the groups past 64 test their box
                 unsigned long long gm = fm & (0x1111111111111111ull << (wave_beam0 >> 6));
                 int b0x = wave_beam0 + 64 * 64;  // groups >= 64 (scans of > 4096 points)
+                if constexpr (S2D_UPD_PRIO) {
+                    // the waves with more of this tile's groups issue first: the four meet at the tile's barrier,
+                    // so the busiest one is the workgroup's path (back to 0 after the raster)
+                    const int c = __popcll(gm);
+                    if (c >= 3) __builtin_amdgcn_s_setprio(3);
+                    else if (c == 2) __builtin_amdgcn_s_setprio(2);
+                    else if (c == 1) __builtin_amdgcn_s_setprio(1);
+                }
                 for (;;) {
                     int b0;
                     if (gm) {
@@ -2338,6 +2357,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     if (k < scnt) upd_mark(lds_ptr(v & 0x3FFFFu), ev);
                 }
             }
+            if (S2D_UPD_PRIO) __builtin_amdgcn_s_setprio(0);
             if (__ballot(anyv != 0u) && lane == 0) s_any[buf] = (unsigned)(i + 1);
         }
         // every pending load first (only LDS work came after them): with the loads conditional the compiler

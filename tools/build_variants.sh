@@ -8,6 +8,8 @@
 #   pk0   round-3 compact-nibble packing of the update's mark bits (S2D_PACK_PERM=0)
 #   ing0  ingest chunk loop for every scan (S2D_ING_PRELOAD=0)
 #   sc0   per-wave miss conversion in the chain-wave match (S2D_CW_SHARECONV=0)
+#   pr0   no raised priority for the match's pre-chain phase (S2D_PRECHAIN_PRIO=0)
+#   uprio update waves prioritised by their share of the tile's fan groups (S2D_UPD_PRIO=1)
 # (round 4's oct / oct2 / wedge / batch / batchw variants were measured slower or equal and removed from the
 # sources; their code is profiles/r04/update_variants_octet_wedge_batch.patch, results profiles/r04/ab_r04f.md, ab_r04g.md)
 set -e
@@ -22,3 +24,5 @@ make -s OUT=../lib/libslam2d_nt.so EXTRA=-DS2D_NT_STORE=1
 make -s OUT=../lib/libslam2d_pk0.so EXTRA=-DS2D_PACK_PERM=0
 make -s OUT=../lib/libslam2d_ing0.so EXTRA=-DS2D_ING_PRELOAD=0
 make -s OUT=../lib/libslam2d_sc0.so EXTRA=-DS2D_CW_SHARECONV=0
+make -s OUT=../lib/libslam2d_pr0.so EXTRA=-DS2D_PRECHAIN_PRIO=0
+make -s OUT=../lib/libslam2d_uprio.so EXTRA=-DS2D_UPD_PRIO=1

@@ -811,6 +811,9 @@ constexpr bool CW_SHARE = S2D_CW_SHARECONV && CW_BUFS == 1;
 #ifndef S2D_PRECHAIN_PRIO
 #define S2D_PRECHAIN_PRIO 2
 #endif
+#ifndef S2D_PROLOGUE_PRIO
+#define S2D_PROLOGUE_PRIO 1  // the kernel's prologue and every level's start at that priority too (0: A/B)
+#endif
 
 template <int NP>
 __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
@@ -1038,6 +1041,8 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     // fused ingest (mi.ranges): the scan's points in beam order to mi.xy_out (for the grid update) and to
     // an LDS copy in nb_val's space, read into registers below before nb_val's first use
     const bool fused = mi.ranges != nullptr;
+    // the prologue (ingest, pose) and every level's start are on the stream's path like a step's pre-chain phase
+    if (S2D_PRECHAIN_PRIO && S2D_PROLOGUE_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);
     load_exptab();
     if (!fused) __syncthreads();  // (fused: the ingest's barriers order the table before its first use)
     const float *scells = cells + (size_t)s * geom.stream_words;
@@ -1108,6 +1113,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             const LevelGeom &g = geom.lv[lvl];
             const int iters = lvl == 0 ? 5 : 3;
             if (n == 0) continue;  // ScanMatcher::matchData returns the hint (ScanMatcher.h:65, :96)
+            if (S2D_PRECHAIN_PRIO && S2D_PROLOGUE_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);
             const float *lc = scells + g.word_offset;
             float est[3], H[9];
             map_from_world(g, tmp, est);

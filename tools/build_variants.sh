@@ -10,6 +10,7 @@
 #   sc0   per-wave miss conversion in the chain-wave match (S2D_CW_SHARECONV=0)
 #   pr0   no raised priority for the match's pre-chain phase (S2D_PRECHAIN_PRIO=0)
 #   uprio update waves prioritised by their share of the tile's fan groups (S2D_UPD_PRIO=1)
+#   pp0   the match prologue / level starts at default priority (S2D_PROLOGUE_PRIO=0)
 # (round 4's oct / oct2 / wedge / batch / batchw variants were measured slower or equal and removed from the
 # sources; their code is profiles/r04/update_variants_octet_wedge_batch.patch, results profiles/r04/ab_r04f.md, ab_r04g.md)
 set -e
@@ -26,3 +27,4 @@ make -s OUT=../lib/libslam2d_ing0.so EXTRA=-DS2D_ING_PRELOAD=0
 make -s OUT=../lib/libslam2d_sc0.so EXTRA=-DS2D_CW_SHARECONV=0
 make -s OUT=../lib/libslam2d_pr0.so EXTRA=-DS2D_PRECHAIN_PRIO=0
 make -s OUT=../lib/libslam2d_uprio.so EXTRA=-DS2D_UPD_PRIO=1
+make -s OUT=../lib/libslam2d_pp0.so EXTRA=-DS2D_PROLOGUE_PRIO=0

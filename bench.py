@@ -134,6 +134,17 @@ def aggregate_over_ranks(elapsed: float, units: float, device):
     return float(el.item()), float(un.item())
 
 
+def launch_ms_max_over_ranks(ktimes: dict, device) -> dict:
+    """Average launch time (ms) of every kernel, MAX over ranks (every rank calls this: a collective)."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([ktimes[k][0] / max(ktimes[k][1], 1) for k in KERNELS], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return dict(zip(KERNELS, t.tolist()))
+
+
 def copy_bandwidth(dev, nbytes=2 << 30, reps=5):
     """Attainable device-to-device copy bandwidth (read + write bytes / time), torch copy_."""
     import torch
@@ -191,6 +202,17 @@ def cpu_baseline(cfg, seconds=10.0, seconds_o0=4.0, thresholds=(-1.0, -1.0)):
                       f"{cfg['levels']} levels, {'forced map update' if thresholds[0] < 0 else 'thresholds 0.4 m / 0.9 rad'}, "
                       "oracle/hector_oracle.c -O3 single thread",
             "value_O0": v0, "sample_O0": f"same stream, first {done0} scans, -O0 build", "cpu_model": cpu_model}
+
+
+def hector_cpu_block(args, cfg, thr, seconds=10.0, seconds_o0=4.0, seconds_all=6.0):
+    """The line's cpu_baseline at EVERY GPU count (north_star: the reference CPU path timed "in the same run"):
+    rank 0 alone runs it, after the timed region, on 1 core and then on --cpu-cores processes."""
+    if args.no_cpu_baseline:
+        return None
+    cpu = cpu_baseline(cfg, seconds=seconds, seconds_o0=seconds_o0, thresholds=thr)
+    if args.cpu_cores > 1:
+        cpu["all_cores"] = cpu_baseline_all_cores(cfg, args.cpu_cores, seconds=seconds_all, thresholds=thr)
+    return cpu
 
 
 def _cpu_stream_worker(args):
@@ -287,19 +309,32 @@ def pose_check(cfg, S, gpu_poses, streams, thresholds=(-1.0, -1.0), order=0):
 def north_star_targets(value, cpu, roof, pose):
     """BASELINE.json north_star's targets, each with its measured value and pass/fail: >= 100x the
     reference CPU path on 1 GPU (against one core, and against all the box's cores used here), >= 40 % of
-    the HBM-read roofline (SURVEY 8d's read model and the counted reads), pose error <= 1e-4 m / rad."""
+    the HBM roofline, pose error <= 1e-4 m / rad.
+    The roofline rows are counted bytes only: the dominant kernel's counted HBM traffic (rocprofv3 FETCH_SIZE x 2
+    + WRITE_SIZE) and its distinct-cell floor (12 B per distinct cell), each over its launch time.  SURVEY 8d's
+    touch model is not a traffic figure (its rate passes the HBM peak, see roofline.survey_8d_note), so it is
+    not a target row.  The north star's "HBM-READ roofline" cannot be met by this workload: the update writes
+    every cell it reads, so counted reads are at most ~39 % of its counted traffic and a read fraction >= 0.40
+    would need more than the HBM peak; read_roofline_counted is reported with that bound beside it."""
     def row(v, target, op, **kw):
         return {"value": None if v is None else round(v, 5), "target": target, "op": op,
                 "pass": None if v is None else bool(v >= target if op == ">=" else v <= target), **kw}
     allc = (cpu or {}).get("all_cores")
+    roof = roof or {}
     return {"x_cpu_1core": row(value / cpu["value"] if cpu else None, 100.0, ">=", cores=1,
                                basis=(cpu or {}).get("kind")),
             "x_cpu_all_cores": row(value / allc["value"] if allc else None, 100.0, ">=",
                                    cores=allc["cores"] if allc else None, basis="port" if allc else None),
-            "read_roofline_model": row((roof or {}).get("read_only_frac"), 0.40, ">=",
-                                       basis="SURVEY 8d read bytes (match gathers + 8 B per cell touch) / step wall time"),
-            "read_roofline_counted": row((roof or {}).get("read_only_frac_counters"), 0.40, ">=",
-                                         basis="rocprofv3 FETCH_SIZE x 2 of the step's kernels / step wall time"),
+            "hbm_roofline_counted": row(roof.get("frac") if roof.get("traffic") else None, 0.40, ">=",
+                                        basis="dominant kernel: counted HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE) per "
+                                              "launch / avg launch time / 8 TB/s"),
+            "hbm_roofline_distinct_cell_floor": row(roof.get("min_traffic_frac"), 0.40, ">=",
+                                                    basis="update: 12 B per distinct cell / avg launch time / 8 TB/s"),
+            "read_roofline_counted": row(roof.get("read_only_frac_counters"), 0.40, ">=",
+                                         basis="rocprofv3 FETCH_SIZE x 2 of the step's kernels / step wall time",
+                                         bound=roof.get("read_share_of_counted"),
+                                         note="cannot pass: counted reads are `bound` of the step's counted traffic, "
+                                              "so even at the HBM peak the read fraction stays below it"),
             "pose_error_m": row(pose["max_abs_xy_m"], 1e-4, "<=", basis="max |GPU - oracle (reference order)|"),
             "pose_error_rad": row(pose["max_abs_theta_rad"], 1e-4, "<=", basis="max |GPU - oracle (reference order)|")}
 
@@ -436,7 +471,7 @@ def run_gmapping(args, world, rank, dev):
                     "traffic": None, "avg_launch_ms": round(kms / kn, 5), "alg_bytes_per_launch": int(alg),
                     "particles_per_launch": P, "free_updates_per_particle": round(float(f.mean()), 1)}
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:  # every GPU count, rank 0 only, after the timed region
             cpu = gmapping_cpu_baseline()
         out = {"metric": GM_METRIC, "value": round(value, 1), "unit": "particle-scans/s", "n_gpus": world, "steps": K,
                "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True, "scaling": "strong",
@@ -529,7 +564,7 @@ def run_plicp(args, world, rank, dev):
     kms, kn = pl.kernel_times(reset=True)
     t_max, total = aggregate_over_ranks(elapsed, float(B * K), dev)
     if rank == 0:
-        cpu = None if (args.no_cpu_baseline or world > 1) else plicp_cpu_baseline()
+        cpu = None if args.no_cpu_baseline else plicp_cpu_baseline()
         out = {"metric": PL_METRIC, "value": round(total / t_max, 1), "unit": "scan-pairs/s", "n_gpus": world,
                "steps": K, "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
@@ -660,7 +695,7 @@ def run_karto(args, world, rank, dev):
     if shard:
         total = float(M * K)  # the same matches on every rank: the job's matches, not the ranks' sum
     if rank == 0:
-        cpu = None if (args.no_cpu_baseline or world > 1) else karto_cpu_baseline(cfg)
+        cpu = None if args.no_cpu_baseline else karto_cpu_baseline(cfg)
         info = sm.info
         coarse_ms, coarse_n = kt.get("kt_coarse_kernel", (0.0, 0))
         nA = 21
@@ -738,8 +773,10 @@ def launcher_selftest(args):
     t0 = time.perf_counter()
     t_max, total = aggregate_over_ranks(time.perf_counter() - t0 + 1e-3, float(args.streams or 1), torch.device("cpu"))
     if rank == 0:
+        # the Hector line's CPU block exactly as main() builds it at any world size (short budgets, c2's grid)
+        cpu = hector_cpu_block(args, CONFIGS["c2"], (-1.0, -1.0), seconds=0.5, seconds_o0=0.2, seconds_all=0.5)
         print(json.dumps({"metric": "launcher-selftest", "value": total / t_max, "unit": "units/s", "n_gpus": world,
-                          "config": {"global_batch": int(total), "ranks": world}}), flush=True)
+                          "config": {"global_batch": int(total), "ranks": world}, "cpu_baseline": cpu}), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
@@ -852,8 +889,14 @@ def main():
     if args.order == "tree":
         fleet.set_reduction_order(HectorFleet.ORDER_TREE256)
     order = fleet.reduction_order()
+    # the source hash compiled into the loaded library (hs_source_id): the line names the binary it timed, and
+    # says whether csrc/ still holds that source (a stale library is marked, not silently attributed)
+    from slam2d import _lib
+    lib_src, tree_src = _lib.source_id_of_library(), kernel_source_id()
+    if lib_src != tree_src:
+        log(f"[bench] WARNING: {_lib.LIB_PATH} was built from Hector sources {lib_src}, csrc/ holds {tree_src}")
     workload = {"config": args.config, "streams": B, "semantics": args.semantics, "order": order,
-                "kernel_src": kernel_source_id(), "issue_split": issue_split()}
+                "kernel_src": lib_src, "issue_split": issue_split()}
     hs = torch.cuda.current_stream(dev).cuda_stream
     # pose log: every 64th stream and the last one (the top of the update lists and of the HBM range)
     log_streams = sorted(set(range(0, B, 64)) | {B - 1})
@@ -934,6 +977,8 @@ def main():
 
     t_max, total_scans = aggregate_over_ranks(elapsed, float(B * K), dev)
     value = total_scans / t_max
+    # per-launch kernel times, MAX over ranks (the roofline's launch time is the slowest rank's)
+    kmax = launch_ms_max_over_ranks(ktimes, dev) if ktimes else None
 
     if rank == 0:
         ab = algorithmic_bytes(ctr, cfg["levels"])
@@ -942,6 +987,7 @@ def main():
             ab_i = algorithmic_bytes(ctr_i, cfg["levels"])
             dom = max(KERNELS, key=lambda k: ktimes[k][0])
             ms, nlaunch = ktimes[dom]
+            ms = kmax[dom] * nlaunch  # the slowest rank's launches (= rank 0's at N = 1)
             avg_s = ms / 1e3 / nlaunch
             ksym = kernel_symbol(dom, ktimes)
             pmc, pmc_why = pmc_traffic(ksym, workload, avg_s * 1e9)
@@ -972,14 +1018,21 @@ def main():
                                        "in LDS and moves each distinct cell once, so this is work, not traffic")
                     if dom == "update" else None,
                     "avg_launch_ms": round(ms / nlaunch, 5),
+                    "avg_launch_ms_basis": "max over ranks" if world > 1 else "rank 0",
                     "timing": "kernel durations from an instrumented pass of K further steps (HIP events "
                               "around each kernel); the headline pass runs without events",
                     "instrumented_ms_per_step": round(elapsed_i / P * 1e3, 4),
                     "kernel_ms_per_step": {k: round(ktimes[k][0] / max(ktimes[k][1], 1), 5) for k in KERNELS},
                     # the north star's "HBM-read roofline": SURVEY 8d's read subset (match gathers + 8 B per cell
-                    # touch) over the step's wall time, and the counted reads of the step's kernels (PMC)
-                    "read_only_frac": round(ab["read_only"] / t_max / 1e9 / HBM_PEAK_GBS, 5),
+                    # touch; a touch model, not traffic) over the step's wall time, and the counted reads of the
+                    # step's kernels (PMC) with their share of the step's counted traffic (the bound on that fraction)
+                    "survey_8d_read_only_frac": round(ab["read_only"] / t_max / 1e9 / HBM_PEAK_GBS, 5),
                     # counted reads per launch x launches per step (ktimes over the P instrumented steps) x K
+                    "read_share_of_counted": (round(2 * (pmc["fetch_kb"] * ktimes["update"][1] + mpmc["fetch_kb"]
+                                                         * ktimes["match"][1]) * 1024
+                                                    / (pmc["traffic_bytes_per_launch"] * ktimes["update"][1]
+                                                       + mpmc["traffic_bytes_per_launch"] * ktimes["match"][1]), 4)
+                                              if (pmc and mpmc and dom == "update") else None),
                     "read_only_frac_counters": (round(2 * (pmc["fetch_kb"] * ktimes["update"][1] + mpmc["fetch_kb"]
                                                            * ktimes["match"][1]) / P * 1024 * K
                                                       / t_max / 1e9 / HBM_PEAK_GBS, 5)
@@ -1004,11 +1057,7 @@ def main():
                         c: ent.get(c) for c in ("insts_valu", "insts_salu", "insts_lds", "wave_cycles", "busy_cycles")}
             if not args.no_copy_probe:
                 roof["attainable_copy_GBps"] = round(copy_bandwidth(dev), 1)
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(cfg, thresholds=thr)
-            if args.cpu_cores > 1:
-                cpu["all_cores"] = cpu_baseline_all_cores(cfg, args.cpu_cores, thresholds=thr)
+        cpu = hector_cpu_block(args, cfg, thr)
         pose = pose_check(cfg, S, d_plog.cpu().numpy(), log_streams, thresholds=thr, order=order)
         out = {"metric": METRIC, "value": round(value, 1), "unit": "scans/s", "n_gpus": world, "steps": K,
                "warmup": W, "ms_per_step": round(t_max / K * 1e3, 4), "higher_is_better": True,
@@ -1027,6 +1076,8 @@ def main():
                                     if pipelined else "one batch call per step"),
                           "parallelism": f"replicas x{world}", "semantics": args.semantics,
                           "reduction_order": order, "kernel_src": workload["kernel_src"],
+                          "kernel_src_of": "hs_source_id() of the loaded library",
+                          "kernel_src_matches_tree": lib_src == tree_src,
                           "issue_split": workload["issue_split"],
                           "map_updates_per_scan": round(ctr["updates"] / max(B * K, 1), 4)},
                "roofline": roof, "cpu_baseline": cpu, "pose_vs_ref": pose}

@@ -491,7 +491,11 @@ int stage_scan(hs_ctx *c, const float *xy, int n, float ox, float oy, const floa
 
 extern "C" {
 
-const char *hs_version(void) { return "slam2d-mi355x hector 0.1 (gfx950)"; }
+#ifndef SLAM2D_SRC_HASH
+#define SLAM2D_SRC_HASH "unknown"  // built outside csrc/Makefile
+#endif
+const char *hs_version(void) { return "slam2d-mi355x hector 0.1 (gfx950) src " SLAM2D_SRC_HASH; }
+const char *hs_source_id(void) { return SLAM2D_SRC_HASH; }
 const char *hs_last_error(void) { return g_err.c_str(); }
 
 int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_x, int map_size_y, float map_start_x,

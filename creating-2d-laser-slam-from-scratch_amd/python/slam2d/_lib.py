@@ -34,6 +34,7 @@ def build(force: bool = False) -> str:
 def _declare(L):
     P = C.POINTER
     L.hs_version.restype = C.c_char_p
+    L.hs_source_id.restype = C.c_char_p
     L.hs_last_error.restype = C.c_char_p
     L.hs_create.argtypes = [P(_p), _i, _f, _i, _i, _f, _f, _i, _i]
     L.hs_destroy.argtypes = [_p]
@@ -111,6 +112,34 @@ def check(rc: int, what: str = "") -> None:
     if rc != 0:
         msg = lib().hs_last_error().decode(errors="replace")
         raise Slam2dError(f"{what} failed with code {rc}: {msg}")
+
+
+def source_id_of_tree() -> str:
+    """16 hex digits of sha256 over the Hector kernel sources in csrc/ (the Makefile's SRC_HASH)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for name in ("hector_kernels.hip", "hector_capi.hip", "hector_internal.h", "detmath.h"):
+        try:
+            with open(os.path.join(CSRC, name), "rb") as f:
+                h.update(f.read())
+        except OSError:
+            return ""
+    return h.hexdigest()[:16]
+
+
+def source_id_of_library() -> str:
+    """The source hash compiled into the loaded library (hs_source_id)."""
+    return lib().hs_source_id().decode()
+
+
+def check_library_matches_tree() -> str:
+    """Raise when the loaded library was built from other Hector sources than csrc/ holds; return the id."""
+    built, tree = source_id_of_library(), source_id_of_tree()
+    if tree and built != tree:
+        raise Slam2dError(f"{LIB_PATH} was built from Hector sources {built}, csrc/ holds {tree}: rebuild it "
+                          f"(__graft_entry__.build())")
+    return built
 
 
 def exported_symbols() -> list[str]:

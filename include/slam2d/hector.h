@@ -46,6 +46,9 @@ typedef struct hs_ctx hs_ctx;
 
 /* Version / self-description of the built library. */
 const char *hs_version(void);
+/* 16 hex digits of sha256 over the Hector kernel sources the library was compiled from (csrc/Makefile
+ * SRC_HASH; bench.py reports it as config.kernel_src and refuses a library that differs from the tree). */
+const char *hs_source_id(void);
 const char *hs_last_error(void);
 
 /* HectorSlamProcessor ctor + MapRepMultiMap ctor (HectorSlamProcessor.h:57-68, MapRepMultiMap.h:57-90).

@@ -147,3 +147,13 @@ def test_cpp_test_host_links_the_product_library():
         pytest.skip("tests/cpp not built")
     out = subprocess.run(["ldd", b], capture_output=True, text=True).stdout
     assert "libslam2d.so => " + REPO in out.replace("tests/cpp/build/../../../", ""), out
+
+
+def test_library_source_id_matches_tree():
+    """The library's compiled-in source hash (hs_source_id, csrc/Makefile SRC_HASH) equals the hash of the Hector
+    sources in csrc/ (bench.py's kernel_src): the prebuilt library that ships to the GPU box is this tree's."""
+    from slam2d import _lib
+
+    built, tree = _lib.source_id_of_library(), _lib.source_id_of_tree()
+    assert len(built) == 16 and built == tree, (built, tree)
+    assert _lib.lib().hs_version().decode().endswith(built)

@@ -254,12 +254,17 @@ def test_bench_gpus_n_launches_its_ranks():
     import sys
 
     r = subprocess.run([sys.executable, os.path.join(bench.REPO, "bench.py"), "--gpus", "2", "--streams", "512",
-                        "--launcher-selftest"], capture_output=True, text=True, timeout=300, env=_bench_env())
+                        "--cpu-cores", "2", "--launcher-selftest"], capture_output=True, text=True, timeout=300,
+                       env=_bench_env())
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 1024, out
+    # the CPU baseline is timed at N > 1 too (rank 0, the same block main() attaches)
+    cpu = out["cpu_baseline"]
+    assert cpu["cores"] == 1 and cpu["value"] > 0 and cpu["kind"] == "port", cpu
+    assert cpu["all_cores"]["cores"] == 2 and cpu["all_cores"]["value"] > 0, cpu
 
 
 def test_bench_world_size_mismatch_is_refused():
@@ -277,13 +282,19 @@ def test_bench_world_size_mismatch_is_refused():
 def test_north_star_targets_block():
     """The bench line's targets block: each target with its value and pass/fail."""
     cpu = {"value": 1000.0, "kind": "port", "all_cores": {"value": 15000.0, "cores": 16}}
-    roof = {"read_only_frac": 0.48, "read_only_frac_counters": 0.12}
+    roof = {"survey_8d_read_only_frac": 0.58, "read_only_frac_counters": 0.14, "read_share_of_counted": 0.387,
+            "frac": 0.455, "traffic": 6650485317, "min_traffic_frac": 0.373}
     pose = {"max_abs_xy_m": 0.0, "max_abs_theta_rad": 0.0}
     t = bench.north_star_targets(1.4e6, cpu, roof, pose)
     assert t["x_cpu_1core"]["value"] == 1400.0 and t["x_cpu_1core"]["pass"]
     assert t["x_cpu_all_cores"]["cores"] == 16 and round(t["x_cpu_all_cores"]["value"], 2) == 93.33
     assert not t["x_cpu_all_cores"]["pass"]
-    assert t["read_roofline_model"]["pass"] and not t["read_roofline_counted"]["pass"]
+    # counted bytes only: SURVEY 8d's touch model is not a target row (its rate can pass the HBM peak)
+    assert "read_roofline_model" not in t
+    assert t["hbm_roofline_counted"]["pass"] and t["hbm_roofline_distinct_cell_floor"]["value"] == 0.373
+    assert not t["read_roofline_counted"]["pass"] and t["read_roofline_counted"]["bound"] == 0.387
+    # without a PMC summary the counted row has no value (the floor fallback is not counted traffic)
+    assert bench.north_star_targets(1.4e6, cpu, {"frac": 0.4, "traffic": None}, pose)["hbm_roofline_counted"]["value"] is None
     assert t["pose_error_m"]["pass"] and t["pose_error_rad"]["pass"]
     assert bench.north_star_targets(1.0, None, None, pose)["x_cpu_1core"]["pass"] is None
 

@@ -13,7 +13,20 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def line(path):
+    """one bench line in brief: value, ms/step, kernel ms, clocks, frac, kernel_src"""
+    d = json.loads([ln for ln in open(path) if ln.startswith("{")][-1])
+    r = d.get("roofline") or {}
+    k = r.get("kernel_ms_per_step") or {}
+    print(os.path.basename(path), round(d["value"]), d["ms_per_step"], k, "sclk", r.get("update_sclk_mhz"),
+          r.get("match_sclk_mhz"), "frac", r.get("frac"), "src", d["config"].get("kernel_src"),
+          "poses", (d.get("pose_vs_ref") or {}).get("exact_frac_vs_reference_order"))
+
+
 def main():
+    if sys.argv[1] == "--line":
+        line(sys.argv[2])
+        return
     tag = sys.argv[1]
     rows = defaultdict(list)
     for p in sorted(glob.glob(os.path.join(REPO, "gpurun_out", f"ab_{tag}_*_*.json"))):

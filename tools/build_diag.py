@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Build a pricing / A-B variant of the product library from a patched COPY of the sources.
 
-  python tools/build_diag.py <variant> [<variant> ...]     -> creating-2d-laser-slam-from-scratch_amd/lib/libslam2d_<variant>.so
+  python tools/build_diag.py <variant> [<variant> ...]     -> creating-2d-laser-slam-from-scratch_amd/lib/ab/libslam2d_<variant>.so
 
 The product sources carry no wrong-result switches: every variant here is a textual patch applied to
 a temporary copy of csrc/ (the build fails loudly if a patch no longer applies).  Variants marked
@@ -115,7 +115,7 @@ def build(variant: str) -> str:
             if text.count(old) != 1:
                 raise SystemExit(f"variant {variant}: patch anchor not found exactly once in {fname}: {old[:60]!r}")
             open(p, "w").write(text.replace(old, new))
-        out = os.path.join(PKG, "lib", f"libslam2d_{variant}.so")
+        out = os.path.join(PKG, "lib", "ab", f"libslam2d_{variant}.so")
         subprocess.check_call(["make", "-s", "-C", src, f"OUT={out}"])
         return out
     finally:

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Compile-time A/B variants of the product library (same sources, other -D switches) next to libslam2d.so:
+# Compile-time A/B variants of the product library (same sources, other -D switches) under lib/ab/ (the driver ships only lib/libslam2d.so; lib/ab/ is gpurun-ignored at round end):
 #   th64  ring update kernel (opt-in, SLAM2D_UPD_KERNEL=ring) with 64-row tiles and 512-thread workgroups
 #   cw2   chain-wave match with two term buffers (S2D_CW_BUFS=2: 38 KB of LDS, 4 workgroups per CU)
 #   r3m   round 3's match chain (S2D_MATCH_CW=0)
@@ -16,15 +16,15 @@
 set -e
 cd "$(dirname "$0")/../creating-2d-laser-slam-from-scratch_amd/csrc"
 make -s
-make -s OUT=../lib/libslam2d_th64.so EXTRA=-DS2D_RING_TH=64
-make -s OUT=../lib/libslam2d_cw2.so EXTRA=-DS2D_CW_BUFS=2
-make -s OUT=../lib/libslam2d_r3m.so EXTRA=-DS2D_MATCH_CW=0
+make -s OUT=../lib/ab/libslam2d_th64.so EXTRA=-DS2D_RING_TH=64
+make -s OUT=../lib/ab/libslam2d_cw2.so EXTRA=-DS2D_CW_BUFS=2
+make -s OUT=../lib/ab/libslam2d_r3m.so EXTRA=-DS2D_MATCH_CW=0
 
-make -s OUT=../lib/libslam2d_noaf.so EXTRA=-DS2D_APPLY_FAST=0
-make -s OUT=../lib/libslam2d_nt.so EXTRA=-DS2D_NT_STORE=1
-make -s OUT=../lib/libslam2d_pk0.so EXTRA=-DS2D_PACK_PERM=0
-make -s OUT=../lib/libslam2d_ing0.so EXTRA=-DS2D_ING_PRELOAD=0
-make -s OUT=../lib/libslam2d_sc0.so EXTRA=-DS2D_CW_SHARECONV=0
-make -s OUT=../lib/libslam2d_pr0.so EXTRA=-DS2D_PRECHAIN_PRIO=0
-make -s OUT=../lib/libslam2d_uprio.so EXTRA=-DS2D_UPD_PRIO=1
-make -s OUT=../lib/libslam2d_pp0.so EXTRA=-DS2D_PROLOGUE_PRIO=0
+make -s OUT=../lib/ab/libslam2d_noaf.so EXTRA=-DS2D_APPLY_FAST=0
+make -s OUT=../lib/ab/libslam2d_nt.so EXTRA=-DS2D_NT_STORE=1
+make -s OUT=../lib/ab/libslam2d_pk0.so EXTRA=-DS2D_PACK_PERM=0
+make -s OUT=../lib/ab/libslam2d_ing0.so EXTRA=-DS2D_ING_PRELOAD=0
+make -s OUT=../lib/ab/libslam2d_sc0.so EXTRA=-DS2D_CW_SHARECONV=0
+make -s OUT=../lib/ab/libslam2d_pr0.so EXTRA=-DS2D_PRECHAIN_PRIO=0
+make -s OUT=../lib/ab/libslam2d_uprio.so EXTRA=-DS2D_UPD_PRIO=1
+make -s OUT=../lib/ab/libslam2d_pp0.so EXTRA=-DS2D_PROLOGUE_PRIO=0

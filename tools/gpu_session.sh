@@ -1,0 +1,46 @@
+#!/bin/bash
+# One GPU session, steps chosen by name, results under gpurun_out/<tag>/ (each step under its own limit,
+# the session stops at the first failure):
+#   tools/gpu_session.sh <tag> <step>...
+#   cold     the driver's exact bench command (python3 bench.py --gpus 1 --steps 20 --warmup 5) -> cold.json
+#            (run it FIRST to time a cold box: no GPU process before it)
+#   pytest   python -m pytest tests -m gpu                                                        -> pytest.log
+#   smoke    __graft_entry__.smoke()                                                              -> smoke.log
+#   warm     the driver's bench command again                                                     -> warm.json
+#   bench:<name>:<args>   bench.py <args> (commas become spaces)                                   -> <name>.json
+#   ab:<lib>,<lib>...     tools/ab_bench.sh over lib/ab/libslam2d_<lib>.so ("main" = the product library)
+#   prof:<name>:<args>    tools/profile_gpu.sh <tag>_<name> <args>
+set -o pipefail
+T=$1; shift
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+O=$R/gpurun_out/$T
+mkdir -p "$O"
+cd "$R"
+for step in "$@"; do
+  case "$step" in
+    cold|warm)
+      timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$O/$step.json" 2> "$O/$step.err" \
+        || { echo "FAIL $step"; tail -20 "$O/$step.err"; exit 1; }
+      python3 tools/ab_summary.py --line "$O/$step.json" ;;
+    pytest)
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1 \
+        || { echo "FAIL pytest"; tail -30 "$O/pytest.log"; exit 1; }
+      tail -2 "$O/pytest.log" ;;
+    smoke)
+      timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
+        || { echo "FAIL smoke"; tail -20 "$O/smoke.log"; exit 1; }
+      tail -1 "$O/smoke.log" ;;
+    bench:*)
+      rest=${step#bench:}; name=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+      timeout -k 10 300 python3 bench.py ${args//,/ } > "$O/$name.json" 2> "$O/$name.err" \
+        || { echo "FAIL $step"; tail -20 "$O/$name.err"; exit 1; }
+      python3 tools/ab_summary.py --line "$O/$name.json" ;;
+    ab:*)
+      libs=${step#ab:}
+      bash tools/ab_bench.sh "$T" ${libs//,/ } || exit 1 ;;
+    prof:*)
+      rest=${step#prof:}; name=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+      bash tools/profile_gpu.sh "${T}_$name" ${args//,/ } || { echo "FAIL $step"; exit 1; } ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -35,11 +35,11 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
                             CONFOUNDED: with no occupied cells the match drifts, so the rays and the tiles they
                             cover change; a hit-bit word map with <= 4 cells per word timed the same as the
                             32-cell half-row words (round 3), i.e. the atomicOr is not what this variant saves
-  seqnochain WRONG RESULTS  hs_match_kernel's sequential sum adds one term per chunk (prices the chain adds;
-                            the chunk hand-offs and barriers stay)
+  seqnochain WRONG RESULTS  hs_match_kernel's chain wave (gn_step_cw, the default) adds one term per chunk (prices
+                            the chain adds; the chunk hand-offs and barriers stay)
   chainregs  WRONG RESULTS  hs_match_kernel's chain reads its first 16 terms from LDS and then re-adds the
                             registers it holds (same adds, no further LDS reads: prices the chain's LDS latency)
-  noprio     same results   hs_match_kernel's chain wave stays at the default wave priority
+  noprio     same results   hs_match_kernel's chain wave (gn_step_cw, the default) stays at the default wave priority
   mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
                             streams per CU)
 """
@@ -83,15 +83,16 @@ PATCHES = {
     "noorigin": [(K, "                    if ((int)!met | (int)(lo_i > hi_i)) continue;\n",
                   "                    if (lo_i < 8) lo_i = 8;\n                    if (!met | (lo_i > hi_i)) continue;\n")],
     "nohitbit": [(K, "                    atomicOr(&hitb[c >> 5], 1u << (c & 31));\n", "                    (void)c;\n")],
-    "seqnochain": [(K, "        if (lane < 9) run = seq_chain(T, lane, cnt, run);",
-                    "        if (lane < 9) run = run + T[lane * SEQ_STRIDE];")],
+    "seqnochain": [(K, "                run = seq_chain_t<CW_STRIDE>(seqT + (CW_BUFS == 2 ? (j & 1) * CW_BUF : 0), lane, min(CW_PTS, n - j * CW_PTS),\n"
+                       "                                             run);\n",
+                    "                run = run + seqT[lane * CW_STRIDE];\n")],
     "frozen": [(K, "            for (int it = 0; it <= iters; ++it) {\n                if (in_regs) {",
                 "            for (int it = 0; it <= iters && false; ++it) {\n                if (in_regs) {")],
     "chainregs": [(K, "            b0 = row[i]; b1 = row[i + 1]; b2 = row[i + 2]; b3 = row[i + 3];\n",
                    "            b0 = a0; b1 = a1; b2 = a2; b3 = a3;\n"),
                   (K, "            a0 = row[i + 4]; a1 = row[i + 5]; a2 = row[i + 6]; a3 = row[i + 7];\n", "")],
-    "noprio": [(K, "        // it issues ahead of the co-resident workgroups' waves (s_setprio; back to 0 after the step tail)\n        __builtin_amdgcn_s_setprio(3);\n",
-                "        // it issues ahead of the co-resident workgroups' waves (s_setprio; back to 0 after the step tail)\n        __builtin_amdgcn_s_setprio(0);\n")],
+    "noprio": [(K, "        // (the workgroup's critical path issues ahead of co-resident workgroups' waves)\n        __builtin_amdgcn_s_setprio(3);\n",
+                "        // (the workgroup's critical path issues ahead of co-resident workgroups' waves)\n        __builtin_amdgcn_s_setprio(0);\n")],
     "mlds3": [(K, "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n",
                "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n"
                "    __shared__ float s_pad[3000];\n    if (stream_begin < 0) s_pad[threadIdx.x] = 1.0f;\n")],

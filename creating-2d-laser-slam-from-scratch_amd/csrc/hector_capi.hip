@@ -510,6 +510,15 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         return fail(HS_EINVAL, "map too small for the requested number of levels");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail(HS_ENODEV, "no HIP device");
+    size_t pad_words = 0;
+    if (const char *sp = getenv("SLAM2D_STREAM_PAD")) {
+        // bytes between streams' pyramids: a non-negative multiple of 256 (whole 64-word granules)
+        char *end = nullptr;
+        const long long v = strtoll(sp, &end, 10);
+        if (end == sp || *end != '\0' || v < 0 || v % 256 != 0 || v > (1ll << 30))
+            return fail(HS_EINVAL, "SLAM2D_STREAM_PAD must be a non-negative multiple of 256 bytes (<= 1 GiB)");
+        pad_words = (size_t)(v / 256) * 64;
+    }
     hs_ctx *c = new hs_ctx();
     c->B = num_streams;
     c->levels = levels;
@@ -519,7 +528,7 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
     c->res = map_resolution;
     c->start_x = map_start_x;
     c->start_y = map_start_y;
-    if (const char *sp = getenv("SLAM2D_STREAM_PAD")) c->stream_pad_words = (size_t)(atoll(sp) / 256) * 64;
+    c->stream_pad_words = pad_words;
     init_geometry(c);
     c->geom.lf = prob_to_logodds(0.4f);  // GridMapLogOddsFunctions ctor (GridMapLogOdds.h:98-102)
     c->geom.lo = prob_to_logodds(0.6f);

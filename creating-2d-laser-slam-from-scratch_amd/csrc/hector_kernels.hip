@@ -1049,9 +1049,12 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     __shared__ int s_w[ING_SW];
     float2 *stage = reinterpret_cast<float2 *>(nb_val);
     const float2 *pts = fused ? mi.xy_out + (size_t)local * xy_stride : xy + (size_t)local * xy_stride;
+    // a caller's count is clamped to [0, max_points] (= mc_stride, the per-stream container's capacity;
+    // hs_step_batch_device documents the range): the register-only instance has no path for more points, and
+    // the update kernel sizes its ray groups by max_points
     const int n = fused ? ingest_scan(ig, mi.cs, mi.ranges + (size_t)local * mi.rstride,
                                       mi.xy_out + (size_t)local * xy_stride, stage, s_w)
-                        : counts[local];
+                        : min(max(counts[local], 0), mc_stride);
 
     float hint[3];
     if (hints) {
@@ -2458,7 +2461,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     clk_stamp(geom.clk, 1, false);
 }
 
-// ------------------------------------ k2 (default, round 4): ring-ordered grid update with ray cursors
+// ------------------------------- k2 (opt-in, SLAM2D_UPD_KERNEL=ring): ring-ordered grid update with ray cursors
+// (the default update is the clip kernel hs_update_kernel above; hector_capi.hip upd_ring_ok)
 // The same once-per-scan update as hs_update_kernel (tiles of 64 x UPD_TH cells, LDS event words + hit
 // bits, the two-stage raster / apply pipeline, fan groups culled per tile with one ballot), with the
 // per-(tile, ray) clip replaced by a cursor per ray.

@@ -105,7 +105,8 @@ int hs_set_map(hs_ctx *ctx, int stream, int level, const float *logodds, const i
 /* ---- batched, device-resident throughput path ------------------------------------------------ */
 /* One HectorSlamProcessor::update for every stream in [stream_begin, stream_begin+count):
  *   d_xy     : device float2 points, stream s at d_xy + 2*xy_stride*(s - stream_begin)
- *   d_n      : device int per stream (0 <= n <= max_points)
+ *   d_n      : device int per stream, 0 <= n <= max_points (the match kernel clamps a count outside that
+ *              range to it: device-side counts are not checked by the host)
  *   d_origo  : device float2 per stream, or NULL for (0,0)
  *   d_hints  : device float3 per stream, or NULL = each stream's last pose
  * Results stay on device; read them with hs_get_poses (synchronising) when needed. */

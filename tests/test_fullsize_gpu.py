@@ -1,6 +1,7 @@
 """GPU parity at the BASELINE.json configs' full sizes (c3 and GMapping at 1024 particles had
 no GPU test, the Karto loop window was tested below its benched size).
 
+  * north star -- the bench's fleet shape, 3840 streams x 2048^2 x 3 levels (161 GB), default issue path;
   * c3  -- lesson4 hector_slam 3-level 4096 x 4096 grid, a fleet of 1024 streams (180 GB of maps, so
            the last stream's cells sit above 2^32 words): streams 0, 511, 512 (the second fleet half of
            hs_run_ranges_device) and 1023 replayed on the oracle, poses every step and every cell of all
@@ -91,6 +92,59 @@ def test_c3_4096x3_fleet_last_stream_bitexact(gpu, monkeypatch, request, pipelin
             assert np.array_equal(m["upd"], ou), (s, lvl)
             assert np.array_equal(_bits(m["logodds"]), _bits(ol)), (s, lvl)
             assert m["update_index"] == o.update_index(lvl), (s, lvl)
+        o.close()
+    fleet.close()
+
+
+def test_north_star_fleet_shape_bitexact(gpu, request):
+    """The bench's own north-star shape (bench.py CONFIGS["northstar"]): 3840 streams x 2048^2 x 3 levels (161 GB
+    of pyramids, three whole rounds of the match at 5 workgroups per CU), raw ranges through
+    hs_run_ranges_device with the default issue path, stream pad and update split, forced map update -- 4 steps.
+    Poses of every 64th stream and the last (the bench's pose log) equal the oracle in the reference order bit for
+    bit at every step, and every cell of all three levels of the first, middle and last streams."""
+    import torch
+
+    B, LV, SIZE, T = 3840, 3, 2048, 4
+    S = synth.make_streams(B, T, seed=5150)
+    nb = S.ranges.shape[2]
+    ang = synth.beam_angles(nb)
+    fleet = HectorFleet(B, 0.05, SIZE, (0.5, 0.5), LV, max_points=1081)
+    request.addfinalizer(fleet.close)  # 161 GB: free it even when an assertion fails
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(-1.0, -1.0)
+    fleet.set_laser(HsLaser.defaults(nb, float(ang[0]), float(ang[1] - ang[0])),
+                    unit_vectors=np.stack([np.cos(ang), np.sin(ang)], 1))
+    logged = sorted(set(range(0, B, 64)) | {B - 1})
+    slot_of = np.full(B, -1, np.int32)
+    slot_of[logged] = np.arange(len(logged), dtype=np.int32)
+    d_slot = torch.from_numpy(slot_of).cuda()
+    d_log = torch.zeros((T, len(logged), 3), dtype=torch.float32, device="cuda")
+    fleet.set_pose_log_slots(d_log.data_ptr(), d_slot.data_ptr(), len(logged), T)
+    d_r = torch.from_numpy(np.ascontiguousarray(S.ranges.transpose(1, 0, 2))).cuda()
+    fleet.run_ranges_device(T, d_r.data_ptr(), nb, B * nb, hip_stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    del d_r
+    log = d_log.cpu().numpy()
+    _, _, did, cells = fleet.poses()
+    assert did.all()
+    full = {0, B // 2, B - 1}
+    for i, s in enumerate(logged + [B // 2]):
+        o = O.HectorOracle(0.05, SIZE, (0.5, 0.5), LV, reduce_threads=T_RED)
+        o.set_update_factors(0.4, 0.9)
+        o.set_thresholds(-1.0, -1.0)
+        for k in range(T):
+            op, _, _ = o.process(S.points[s, k, : S.counts[s, k]])
+            if slot_of[s] >= 0:
+                got = log[k, slot_of[s]]
+                assert np.array_equal(_bits(got), _bits(op)), (s, k, got, op)
+        assert cells[s] == o.sum_L(), s
+        if s in full:
+            for lvl in range(LV):
+                m = fleet.get_map(s, lvl)
+                ol, ou = o.level(lvl)
+                assert np.array_equal(m["upd"], ou), (s, lvl)
+                assert np.array_equal(_bits(m["logodds"]), _bits(ol)), (s, lvl)
+                assert m["update_index"] == o.update_index(lvl), (s, lvl)
         o.close()
     fleet.close()
 

@@ -149,13 +149,20 @@ def test_step_ranges_matches_oracle_pipeline(gpu):
             assert np.array_equal(_bits(m["logodds"]), _bits(ol))
 
 
-def test_step_ranges_wide_scan_separate_ingest(gpu):
-    """Scans of more than 1280 beams do not fit the match kernel's registers: the ingest runs as its own
-    kernel and the match takes its strided path -- still equal to oracle.ingest -> oracle process."""
+@pytest.mark.parametrize("NB,lo,hi", [(1440, 1280, 1440), (1200, 1152, 1280)])
+def test_step_ranges_wide_scan_separate_ingest(gpu, NB, lo, hi):
+    """Scans past the match kernel's register slots, in the reference order (the chain-wave match keeps
+    <= 1152 points in registers):
+    * 1440 beams (> 1280): the ingest runs as its own kernel and the match takes its strided HBM path;
+    * 1200 beams, ranges clipped below 20 m so that 1153..1280 points survive the node's filters: the ingest
+      stays fused into the match kernel (<= 1280 beams), whose non-register instance (max_points > 1152) then
+      reads the points the same kernel's ingest wrote to HBM.
+    Both equal oracle.ingest -> oracle process bit for bit."""
     import torch
-    NB = 1440
     S, T, LV, SIZE = 2, 6, 2, 512
     scans = synth.make_streams(S, T, with_points=False, seed=3, n_beams=NB)
+    if NB <= 1280:
+        scans.ranges[:] = np.minimum(scans.ranges, np.float32(19.5))
     ang = synth.beam_angles(NB)
     L = HsLaser.defaults(NB, float(ang[0]), float(ang[1] - ang[0]))
     cs = np.ascontiguousarray(np.stack([np.cos(ang), np.sin(ang)], 1))
@@ -175,7 +182,7 @@ def test_step_ranges_wide_scan_separate_ingest(gpu):
         gp, _, gd, _ = fleet.poses()
         for s in range(S):
             pts, org = O.ingest(r[s], cs, L.as_oracle_dict(), scale)
-            assert pts.shape[0] > 1280  # the wide path
+            assert lo < pts.shape[0] <= hi, pts.shape[0]  # the path under test
             op, _, od = oras[s].process(pts, origo=tuple(org))
             assert gd[s] == od, (t, s)
             assert np.array_equal(_bits(gp[s]), _bits(op)), (t, s, gp[s], op)

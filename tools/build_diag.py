@@ -40,6 +40,12 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
   chainregs  WRONG RESULTS  hs_match_kernel's chain reads its first 16 terms from LDS and then re-adds the
                             registers it holds (same adds, no further LDS reads: prices the chain's LDS latency)
   noprio     same results   hs_match_kernel's chain wave (gn_step_cw, the default) stays at the default wave priority
+  noload     WRONG RESULTS  hs_update_kernel applies its marks to zeros instead of loading the marked quads (prices the
+                            apply's load latency, exposed once per tile when the raster before it is short)
+  nostore    WRONG RESULTS  hs_update_kernel computes the apply but stores nothing (prices the write traffic)
+  noidx      WRONG RESULTS  hs_update_kernel stores no updateIndex (log-odds exact: prices the index plane's stores)
+  idx16      WRONG RESULTS  hs_update_kernel stores the updateIndex as 16-bit values in the first half of the index plane
+                            (log-odds exact: prices a 16-bit scan-ordinal plane's stores)
   mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
                             streams per CU)
 """
@@ -96,6 +102,26 @@ PATCHES = {
     "mlds3": [(K, "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n",
                "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n"
                "    __shared__ float s_pad[3000];\n    if (stream_begin < 0) s_pad[threadIdx.x] = 1.0f;\n")],
+    "noload": [(K, "                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));\n",
+                "                    if (mk) ql[j] = make_float4(0.0f, 0.0f, 0.0f, (float)row);\n")],
+    "nostore": [(K, "__device__ __forceinline__ void upd_store(float4 *p, float4 v)\n{\n#if S2D_NT_STORE",
+                 "__device__ __forceinline__ void upd_store(float4 *p, float4 v)\n{\n    if (v.x == 1234.5f) *p = v;\n    return;\n#if S2D_NT_STORE"),
+                (K, "__device__ __forceinline__ void upd_store(int4 *p, int4 v)\n{\n#if S2D_NT_STORE",
+                 "__device__ __forceinline__ void upd_store(int4 *p, int4 v)\n{\n    if (v.x == 1234) *p = v;\n    return;\n#if S2D_NT_STORE"),
+                (K, "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n#if S2D_NT_STORE",
+                 "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n    if (v == 1234) *p = v;\n    return;\n#if S2D_NT_STORE")],
+    "noidx": [(K, "                if (qb_all(mb)) {\n                    upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) upd_store(&tu[o + (unsigned)c], uv[c]);\n                }\n", "")],
+    "idx16": [(K, "                if (qb_all(mb)) {\n                    upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) upd_store(&tu[o + (unsigned)c], uv[c]);\n                }\n",
+               "                {\n"
+               "                    unsigned short *tu16 = reinterpret_cast<unsigned short *>(tu);\n"
+               "                    if (qb_all(mb)) {\n"
+               "                        *reinterpret_cast<uint2 *>(&tu16[o]) = make_uint2((unsigned)(uv[0] & 0xFFFF) | ((unsigned)uv[1] << 16), (unsigned)(uv[2] & 0xFFFF) | ((unsigned)uv[3] << 16));\n"
+               "                    } else {\n"
+               "#pragma unroll\n"
+               "                        for (int c = 0; c < 4; ++c)\n"
+               "                            if (qb_cell(mb, c)) tu16[o + (unsigned)c] = (unsigned short)uv[c];\n"
+               "                    }\n"
+               "                }\n")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

@@ -102,6 +102,9 @@ struct hs_ctx {
     // half's match.  Measured slower at the north-star size (0.97 M vs 1.04 M scans/s: the update
     // kernel already fills the CUs, and a concurrent match slows it more than it hides), so off by default.
     bool pipeline = false;
+    // ordinal sweep (hector_internal.h ORD_OFF): steps since the last one, and the interval (SLAM2D_ORD_SWEEP, tests)
+    int ord_steps = 0;
+    int ord_interval = ORD_SWEEP_MAX;
     bool fuse_ingest = true;  // range arrays: ingest inside the match kernel (SLAM2D_FUSE_INGEST=0: own kernel)
     // Hessian summation order of hs_match_kernel: 0 = the reference's sequential point order (default),
     // 256 = the 256-thread tree (hs_set_reduction_order / SLAM2D_MATCH_ORDER=tree)
@@ -396,11 +399,28 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     return HS_OK;
 }
 
+// Before every step that can update the maps: every ord_interval steps, move all streams' hot ordinals into the
+// cold updateIndex plane and advance their epochs (a step advances a stream's update ordinal by at most one, so
+// 2 (k - E) + 2 stays below 2^16).  On stream s, after the previous steps and before this one.
+int ord_sweep_if_due(hs_ctx *c, hipStream_t s)
+{
+    if (++c->ord_steps <= c->ord_interval) return HS_OK;
+    const int tiles = (int)(c->geom.cells_words / TILE_BLOCK_WORDS);
+    hipLaunchKernelGGL(hs_ord_sweep_kernel, dim3(4096), dim3(256), 0, s, c->d_cells, c->d_state, c->geom.stream_words,
+                       tiles, 0, c->B);
+    HCHK(hipGetLastError());
+    hipLaunchKernelGGL(hs_ord_epoch_kernel, dim3((c->B + 255) / 256), dim3(256), 0, s, c->d_state, 0, c->B);
+    HCHK(hipGetLastError());
+    c->ord_steps = 1;
+    return HS_OK;
+}
+
 int launch_step(hs_ctx *c, int begin, int count, const float2 *xy, int xy_stride, const int *n, const float2 *origo,
                 const float *hints, int mode, float *out_pose, float *out_cov, hipStream_t s,
                 const MatchIngest *mi = nullptr)
 {
     if (count <= 0) return HS_OK;
+    if (mode != MODE_MATCH_ONLY && ord_sweep_if_due(c, s) != HS_OK) return HS_EHIP;
     const int parts = (mode == MODE_PROCESS && count >= 64 * c->nparts) ? c->nparts : 1;
     if (parts == 1)
         return launch_part(c, 0, begin, count, xy, xy_stride, n, origo, hints, mode, out_pose, out_cov, s, nullptr, mi);
@@ -579,6 +599,11 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         c->reduce_order = (mo && strcmp(mo, "tree") == 0) ? MATCH_THREADS : 0;
         const char *fi = getenv("SLAM2D_FUSE_INGEST");
         c->fuse_ingest = !(fi && atoi(fi) == 0);
+        // steps between ordinal sweeps (tests set a few to exercise the sweep; at most ORD_SWEEP_MAX)
+        if (const char *os = getenv("SLAM2D_ORD_SWEEP")) {
+            const int v = atoi(os);
+            c->ord_interval = v < 1 ? 1 : (v > ORD_SWEEP_MAX ? ORD_SWEEP_MAX : v);
+        }
         const char *np = getenv("SLAM2D_PARTS");
         c->nparts = np ? atoi(np) : 1;
         const char *um = getenv("SLAM2D_UPDATE");
@@ -869,7 +894,15 @@ int hs_get_map(hs_ctx *c, int stream, int level, int8_t *occ_out, float *logodds
             for (int x = 0; x < L.sx; ++x) {
                 const size_t w = cell_word(L, x, y), o = (size_t)y * L.sx + x;
                 if (logodds_out) logodds_out[o] = tmp[w];
-                if (upd_out) memcpy(&upd_out[o], &tmp[w + TILE_CELLS], sizeof(int32_t));
+                if (upd_out) {
+                    // the hot ordinal when set (hector_internal.h ORD_OFF), else the cold updateIndex
+                    const size_t tb = w - (size_t)tile_cell(x % TILE, y % TILE_H);  // the tile block
+                    const size_t ci = w - tb;
+                    uint16_t h;
+                    memcpy(&h, reinterpret_cast<const char *>(&tmp[tb + ORD_OFF]) + 2 * ci, sizeof(h));
+                    if (h) upd_out[o] = ord_index(h, st.ord_epoch);
+                    else memcpy(&upd_out[o], &tmp[tb + COLD_OFF + ci], sizeof(int32_t));
+                }
             }
     }
     if (update_index_out) *update_index_out = st.map_updates - 1;
@@ -892,7 +925,10 @@ int hs_set_map(hs_ctx *c, int stream, int level, const float *logodds, const int
         for (int x = 0; x < L.sx; ++x) {
             const size_t w = cell_word(L, x, y), o = (size_t)y * L.sx + x;
             tmp[w] = logodds[o];
-            memcpy(&tmp[w + TILE_CELLS], &upd[o], sizeof(int32_t));
+            const size_t tb = w - (size_t)tile_cell(x % TILE, y % TILE_H), ci = w - tb;
+            memcpy(&tmp[tb + COLD_OFF + ci], &upd[o], sizeof(int32_t));   // the cold plane ...
+            const uint16_t zero = 0;
+            memcpy(reinterpret_cast<char *>(&tmp[tb + ORD_OFF]) + 2 * ci, &zero, sizeof(zero));  // ... in effect
         }
     HCHK(hipMemcpyAsync(base, tmp.data(), sizeof(float) * nwords, hipMemcpyHostToDevice, c->stream));
     HCHK(hipStreamSynchronize(c->stream));
@@ -942,6 +978,18 @@ int hs_run_ranges_device(hs_ctx *c, int steps, const float *d_ranges, int range_
     for (int h = 0; h < 2; ++h) HCHK(hipStreamWaitEvent(c->pstream[h], c->ev_start, 0));
     for (int k = 0; k < steps && rc == HS_OK; ++k) {
         const float *rk = d_ranges + (size_t)k * step_stride;
+        if (c->ord_steps + 1 > c->ord_interval) {
+            // an ordinal sweep is due: after both halves' previous updates, before either half's next step
+            for (int h = 0; h < 2; ++h) {
+                HCHK(hipEventRecord(c->ev_done[h], c->pstream[h]));
+                HCHK(hipStreamWaitEvent(s, c->ev_done[h], 0));
+            }
+            if ((rc = ord_sweep_if_due(c, s)) != HS_OK) break;
+            HCHK(hipEventRecord(c->ev_start, s));
+            for (int h = 0; h < 2; ++h) HCHK(hipStreamWaitEvent(c->pstream[h], c->ev_start, 0));
+        } else {
+            ++c->ord_steps;
+        }
         for (int h = 0; h < 2 && rc == HS_OK; ++h) {
             hipStream_t ps = c->pstream[h];
             float2 *xy = c->d_ixy + (size_t)beg[h] * c->max_points;

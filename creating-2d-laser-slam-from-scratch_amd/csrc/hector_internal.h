@@ -10,15 +10,36 @@ constexpr int MAX_LEVELS = 8;
 constexpr int MATCH_THREADS = 256;
 constexpr int MATCH_WAVES = MATCH_THREADS / 64;
 // Cell storage is tiled: a level is a grid of TILE x TILE_H tiles (padded up), each tile one
-// contiguous 16 KB block = 2048 log-odds floats (4 x 4-cell blocks, see tile_cell) followed by the 2048
-// matching updateIndex ints.  A tile is exactly the unit the grid-update kernel reads and writes.
+// contiguous 20 KB block of three planes, cells in the same order in each (4 x 4-cell blocks, see tile_cell):
+//   [0, TILE_CELLS)             log-odds floats (LogOddsCell::logOddsVal)
+//   [ORD_OFF, +TILE_CELLS / 2)  16-bit update ordinals ("hot" updateIndex, written by every grid update)
+//   [COLD_OFF, +TILE_CELLS)     32-bit updateIndex ints ("cold": written only by the ordinal sweep and hs_set_map)
+// LogOddsCell::updateIndex (GridMapLogOdds.h:85-86) of a cell is read from the hot plane when its ordinal h is
+// non-zero -- the last update k that touched it, h = 2 (k - E) + 1 + hit, E the stream's ordinal epoch, so the
+// index is 3 (E + (h - 1) / 2) + 1 + (h - 1) % 2 = currMarkFreeIndex / currMarkOccIndex of update k
+// (OccGridMapBase.h:120-121, 167: currUpdateIndex = 3 k) -- and from the cold plane otherwise.  Every
+// ORD_SWEEP_MAX steps at most, hs_ord_sweep_kernel moves every non-zero ordinal into the cold plane and advances
+// E, so h never overflows 16 bits.  The grid update thus writes 2 B of index per marked cell instead of 4
+// (round 5: the 4-B index stores were a quarter of hs_update_kernel's time).
+// A tile is exactly the unit the grid-update kernel reads and writes.
 #ifndef S2D_TILE_H
 #define S2D_TILE_H 32
 #endif
 constexpr int TILE = 64;
 constexpr int TILE_H = S2D_TILE_H;
 constexpr int TILE_CELLS = TILE * TILE_H;   // 2048 at 64 x 32
-constexpr int TILE_BLOCK_WORDS = 2 * TILE_CELLS;
+constexpr int ORD_OFF = TILE_CELLS;                    // 4-byte word offset of the 16-bit ordinal plane
+constexpr int COLD_OFF = TILE_CELLS + TILE_CELLS / 2;   // 4-byte word offset of the 32-bit index plane
+constexpr int TILE_BLOCK_WORDS = COLD_OFF + TILE_CELLS;
+constexpr int ORD_SWEEP_MAX = 32000;  // steps between ordinal sweeps at most (h <= 2 * 32000 + 1 < 2^16)
+// updateIndex of a cell from its hot ordinal h (!= 0) and the stream's ordinal epoch E
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline int ord_index(unsigned h, int epoch)
+{
+    return 3 * (epoch + (int)((h - 1u) >> 1)) + 1 + (int)((h - 1u) & 1u);
+}
 
 enum StepMode : int {
     MODE_PROCESS = 0,        // HectorSlamProcessor::update
@@ -61,7 +82,7 @@ inline int tile_cell(int lx, int ly)  // (lx, ly) inside the tile (>= 0) -> its 
                  (x % CELL_BLK));
 }
 
-// word index of cell (x, y)'s log-odds inside its level; its updateIndex is TILE_CELLS words later
+// word index of cell (x, y)'s log-odds inside its level (its ordinal and index: ORD_OFF / COLD_OFF planes, above)
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
@@ -107,6 +128,8 @@ struct alignas(16) StreamState {
     unsigned long long tot_steps;     // steps
     unsigned long long tot_touched;   // distinct cells written by the grid update (Σ levels, per scan)
     int step_index;                   // steps since hs_reset (pose-log row)
+    int ord_epoch;                    // E: update ordinal of the last ordinal sweep (see ORD_OFF)
+    int ord_base;                     // this step's hot ordinal of a freed cell, 2 (k - E) + 1 (+1: occupied)
     // MapRepMultiMap::dataContainers (MapRepMultiMap.h:89, :161): the DataContainer of the last
     // matchData, which updateByScan draws into levels >= 1 (:187).  Its points (level-0 scale) live in
     // the context's per-stream container buffer; empty (mc_n = 0) until the first match.

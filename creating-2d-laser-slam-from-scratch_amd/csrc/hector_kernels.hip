@@ -1218,6 +1218,9 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
         st.upd_pose[1] = np_[1];
         st.upd_pose[2] = np_[2];
         st.mark_base = st.cur_update_index;  // currMarkFreeIndex = +1, currMarkOccIndex = +2 (OccGridMapBase.h:120-121)
+        // the hot ordinal of this update k = currUpdateIndex / 3 (hector_internal.h ORD_OFF): freed cells get
+        // 2 (k - E) + 1, occupied ones + 1
+        st.ord_base = 2 * (st.cur_update_index / 3 - st.ord_epoch) + 1;
         st.cur_update_index += 3;            // OccGridMapBase.h:167
         st.map_updates += 1;                 // GridMapBase::setUpdated (GridMapBase.h:333)
         st.step_cells = 0;
@@ -1575,7 +1578,7 @@ hs_bin_kernel(FleetGeom geom, StreamState *__restrict__ state, const float2 *__r
                     it.begin_xy = begin_xy;
                     it.seg_begin = 0;
                     it.seg_count = 0;
-                    it.mark_base = (unsigned)st.mark_base;
+                    it.mark_base = (unsigned)st.ord_base;
                     it.n = 0;
                     items[idx] = it;
                 }
@@ -1593,7 +1596,7 @@ hs_bin_kernel(FleetGeom geom, StreamState *__restrict__ state, const float2 *__r
                         it.begin_xy = begin_xy;
                         it.seg_begin = seg_base + (unsigned)seg_pre;
                         it.seg_count = (unsigned)c;
-                        it.mark_base = (unsigned)st.mark_base;
+                        it.mark_base = (unsigned)st.ord_base;
                         it.n = s_rows[t];  // tile items: touched-row mask
                         items[item_base + (unsigned)ne_pre] = it;
                         ++ne_pre;
@@ -1622,7 +1625,7 @@ hs_bin_kernel(FleetGeom geom, StreamState *__restrict__ state, const float2 *__r
             it.begin_xy = begin_xy;
             it.seg_begin = (unsigned)ntx | ((unsigned)nty << 16);
             it.seg_count = 0;
-            it.mark_base = (unsigned)st.mark_base;
+            it.mark_base = (unsigned)st.ord_base;
             it.n = (unsigned)n;
             wholes[k] = it;
         }
@@ -1707,8 +1710,9 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
         const int lvl = item.lvl_kind & 0xFF;
         const int kind = item.lvl_kind >> 8;
         const LevelGeom &g = geom.lv[lvl];
-        const int mark_free = (int)item.mark_base + 1;  // currMarkFreeIndex (:120)
-        const int mark_occ = (int)item.mark_base + 2;   // currMarkOccIndex  (:121)
+        // hot ordinals of currMarkFreeIndex / currMarkOccIndex (:120-121; hector_internal.h ORD_OFF)
+        const unsigned short mark_free = (unsigned short)item.mark_base;
+        const unsigned short mark_occ = (unsigned short)(item.mark_base + 1u);
         float *lvw = cells + (size_t)s * geom.stream_words + g.word_offset;
         const int x0 = (int)(item.begin_xy & 0xFFFFu), y0 = (int)(item.begin_xy >> 16);
         const int ttx0 = (int)(item.tile_xy & 0xFFFFu), tty0 = (int)(item.tile_xy >> 16);
@@ -1727,9 +1731,9 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
             const int X0 = (ttx0 + tt % ntx) * TILE, Y0 = (tty0 + tt / ntx) * TILE_H;
             const int gx = X0 + lane;
             const bool colok = gx < g.sx;
-            // this tile's contiguous 16 KB block: log-odds plane then updateIndex plane
+            // this tile's contiguous block: log-odds plane, then the 16-bit ordinal plane
             float *tl = lvw + (size_t)((ttx0 + tt % ntx) + (tty0 + tt / ntx) * g.tiles_x) * TILE_BLOCK_WORDS;
-            int *tu = reinterpret_cast<int *>(tl + TILE_CELLS);
+            unsigned short *tu = reinterpret_cast<unsigned short *>(tl + ORD_OFF);
             float cl[TILE_H];
 #pragma unroll
             for (int row = 0; row < TILE_H; ++row) {
@@ -1819,7 +1823,7 @@ hs_tile_kernel(FleetGeom geom, float *__restrict__ cells, const StreamState *__r
                     const bool fre = (fk & 0xFFFF0000u) == gkey;
                     if (!hit && !fre) continue;
                     float l = cl[row];
-                    int upd;
+                    unsigned short upd;
                     if (!hit) {
                         l = l + lf;        // updateSetFree (GridMapLogOdds.h:120-124)
                         upd = mark_free;
@@ -2201,8 +2205,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     }
     const int tx0 = s_bbox[0] / TILE, ty0 = s_bbox[1] / UPD_TH;
     const int tx1 = s_bbox[2] / TILE, ty1 = s_bbox[3] / UPD_TH;
-    const int mark_free = st.mark_base + 1;  // currMarkFreeIndex (:120)
-    const int mark_occ = st.mark_base + 2;   // currMarkOccIndex  (:121)
+    // hot ordinals of currMarkFreeIndex (:120) / currMarkOccIndex (:121): hector_internal.h ORD_OFF
+    const unsigned mark_free = (unsigned)st.ord_base;  // (+1: currMarkOccIndex, the hit bit added per cell)
     const float lf = geom.lf, lo = geom.lo;
     unsigned touched = 0;
 
@@ -2377,10 +2381,10 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
         // i.e. a wait for all of this apply's stores.
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         if (pend_tl) {
-            // apply the previous tile: log-odds of every marked cell, both planes written (see below);
-            // the updateIndex plane is never read --
-            // a cell's stored index always predates this scan's marks (currUpdateIndex += 3 per scan)
-            int *tu = reinterpret_cast<int *>(pend_tl + TILE_CELLS);
+            // apply the previous tile: log-odds of every marked cell, and its hot ordinal (see below); the
+            // ordinal plane is never read -- a cell's stored index always predates this scan's marks
+            // (currUpdateIndex += 3 per scan)
+            unsigned short *tu = reinterpret_cast<unsigned short *>(pend_tl + ORD_OFF);
 #pragma unroll
             for (int j = 0; j < UPD_QUADS; ++j) {
                 const unsigned mb = qb[j];
@@ -2390,7 +2394,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
-                int uv[4];
+                unsigned uv[4];
                 if (S2D_APPLY_FAST && !__any(qb_hits(mb))) {
                     // no end cell in this quad slot of the whole wave (about three quarters of level 0's on the
                     // synthetic scans): every marked cell is free only -- updateSetFree alone, two VALU per cell
@@ -2411,19 +2415,19 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                         const float h = bit_select(mb, qb_od(c), u, l);  // an earlier beam freed the hit cell
                         const float oc = h < 50.0f ? h + lo : h;         // updateSetOccupied
                         nv[c] = qb_sel_marked(mb, c, bit_select(mb, qb_hit(c), oc, t), l);
-                        uv[c] = __float_as_int(bit_select(mb, qb_hit(c), __int_as_float(mark_occ), __int_as_float(mark_free)));
+                        uv[c] = mark_free + ((mb >> qb_hit(c)) & 1u);
                     }
                 }
                 // log-odds: the whole quad was loaded, so it is stored whole (one instruction; unmarked
-                // cells rewrite their own value); updateIndex: whole when every cell is marked, else
+                // cells rewrite their own value); ordinals: the quad's 8 bytes when every cell is marked, else
                 // per marked cell (its unmarked cells were never read)
                 upd_store(reinterpret_cast<float4 *>(&pend_tl[o]), make_float4(nv[0], nv[1], nv[2], nv[3]));
                 if (qb_all(mb)) {
-                    upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));
+                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));
                 } else {
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        if (qb_cell(mb, c)) upd_store(&tu[o + (unsigned)c], uv[c]);
+                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];
                 }
                 touched += qb_count(mb);
             }
@@ -2876,8 +2880,8 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
     const int my_tiles = tiles_within(ke - 1, ox, oy, tx0, tx1, ty0, ty1) - tiles_within(kb - 1, ox, oy, tx0, tx1, ty0, ty1);
 #pragma unroll
     for (int k = 0; k < RING_GROUPS; ++k) Sk[k] = ray_cursor(Ck[k], kb, x0, y0, ox, oy);
-    const int mark_free = st.mark_base + 1;  // currMarkFreeIndex (:120)
-    const int mark_occ = st.mark_base + 2;   // currMarkOccIndex  (:121)
+    // hot ordinals of currMarkFreeIndex (:120) / currMarkOccIndex (:121): hector_internal.h ORD_OFF
+    const unsigned mark_free = (unsigned)st.ord_base;  // (+1: currMarkOccIndex, the hit bit added per cell)
     const float lf = geom.lf, lo = geom.lo;
     unsigned touched = 0;
     const int nfans = ((n + RTHREADS - 1) / RTHREADS) * (RTHREADS / 64);
@@ -2934,7 +2938,7 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): see hs_update_kernel
         if (pend_tl) {
-            int *tu = reinterpret_cast<int *>(pend_tl + TILE_CELLS);
+            unsigned short *tu = reinterpret_cast<unsigned short *>(pend_tl + ORD_OFF);
             // the quads' offsets are recomputed per tile from an opaque copy of tid (a few VALU): hoisted out of
             // the tile loop they were held in registers the cursors need, and spilled
             int tq = tid;
@@ -2948,7 +2952,7 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
-                int uv[4];
+                unsigned uv[4];
                 if (S2D_APPLY_FAST && !__any((mb >> 8) & 15u)) {
                     // no end cell in this quad slot of the whole wave (three quarters of level 0's, tools'
                     // density model): every marked cell is free only -- updateSetFree alone
@@ -2966,16 +2970,16 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
                         const float h = bit_select(mb, 4 + c, u, l);  // an earlier beam freed the hit cell
                         const float oc = h < 50.0f ? h + lo : h;      // updateSetOccupied
                         nv[c] = bit_select(mb, c, bit_select(mb, 8 + c, oc, t), l);
-                        uv[c] = __float_as_int(bit_select(mb, 8 + c, __int_as_float(mark_occ), __int_as_float(mark_free)));
+                        uv[c] = mark_free + ((mb >> (8 + c)) & 1u);
                     }
                 }
                 *reinterpret_cast<float4 *>(&pend_tl[o]) = make_float4(nv[0], nv[1], nv[2], nv[3]);
                 if ((mb & 15u) == 15u) {
-                    *reinterpret_cast<int4 *>(&tu[o]) = make_int4(uv[0], uv[1], uv[2], uv[3]);
+                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));
                 } else {
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        if ((mb >> c) & 1u) tu[o + (unsigned)c] = uv[c];
+                        if ((mb >> c) & 1u) tu[o + (unsigned)c] = (unsigned short)uv[c];
                 }
                 touched += __popc(mb & 15u);
             }
@@ -3022,16 +3026,18 @@ hs_update_ring_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__
 // --------------------------------------------------------------------------- utility kernels
 __global__ void hs_fill_cells_kernel(float *__restrict__ words, size_t n, size_t stream_words)
 {
-    // LogOddsCell::resetGridCell  H/map/GridMapLogOdds.h:76-80 : log-odds plane 0.0f, updateIndex plane -1.
-    // The plane of a word follows from its offset inside its stream (levels start at multiples of a tile
-    // block; a per-stream pad, if any, is filled too and never read)
+    // LogOddsCell::resetGridCell  H/map/GridMapLogOdds.h:76-80 : log-odds plane 0.0f, updateIndex -1 (the cold
+    // plane -1, the hot ordinal plane 0 = "see the cold plane").  The plane of a word follows from its offset
+    // inside its stream (levels start at multiples of a tile block; a per-stream pad, if any, is filled too and
+    // never read)
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     size_t stream = i / stream_words, w = i - stream * stream_words;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     const size_t ds = stride / stream_words, dw = stride - ds * stream_words;
     for (; i < n; i += stride) {
-        if ((w / TILE_CELLS) & 1) reinterpret_cast<int *>(words)[i] = -1;
-        else words[i] = 0.0f;
+        const unsigned tw = (unsigned)(w % (size_t)TILE_BLOCK_WORDS);
+        if (tw >= (unsigned)COLD_OFF) reinterpret_cast<int *>(words)[i] = -1;
+        else words[i] = 0.0f;  // log-odds 0.0f, and two zero ordinals per word
         w += dw;  // (stream, w) of i + stride without a division per word
         stream += ds;
         if (w >= stream_words) {
@@ -3039,6 +3045,38 @@ __global__ void hs_fill_cells_kernel(float *__restrict__ words, size_t n, size_t
             ++stream;
         }
     }
+}
+
+// Ordinal sweep (hector_internal.h ORD_OFF): every non-zero hot ordinal of streams [stream_begin, +count) becomes
+// its cell's updateIndex in the cold plane and is cleared; hs_ord_epoch_kernel then advances the streams' epochs.
+// One workgroup per tile block (grid-stride); two ordinals per 4-byte word.
+__global__ void __launch_bounds__(256) hs_ord_sweep_kernel(float *__restrict__ cells, const StreamState *__restrict__ state,
+                                                           size_t stream_words, int tiles_per_stream, int stream_begin,
+                                                           int count)
+{
+    const size_t nblk = (size_t)count * (size_t)tiles_per_stream;
+    for (size_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const int s = stream_begin + (int)(b / (size_t)tiles_per_stream);
+        const size_t t = b % (size_t)tiles_per_stream;
+        float *tl = cells + (size_t)s * stream_words + t * TILE_BLOCK_WORDS;
+        unsigned *hot = reinterpret_cast<unsigned *>(tl + ORD_OFF);
+        int *cold = reinterpret_cast<int *>(tl + COLD_OFF);
+        const int E = state[s].ord_epoch;
+        for (int w = threadIdx.x; w < TILE_CELLS / 2; w += blockDim.x) {
+            const unsigned hw = hot[w];
+            if (!hw) continue;
+            const unsigned h0 = hw & 0xFFFFu, h1 = hw >> 16;
+            if (h0) cold[2 * w] = ord_index(h0, E);
+            if (h1) cold[2 * w + 1] = ord_index(h1, E);
+            hot[w] = 0u;
+        }
+    }
+}
+
+__global__ void hs_ord_epoch_kernel(StreamState *__restrict__ state, int stream_begin, int count)
+{
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < count) state[stream_begin + i].ord_epoch = state[stream_begin + i].cur_update_index / 3;
 }
 
 // HectorMappingRos::publishMap cell conversion  lesson4/src/hector_mapping/hector_slam.cc:287-304

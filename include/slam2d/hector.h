@@ -173,9 +173,12 @@ int hs_get_counters(hs_ctx *ctx, int64_t out[6], int reset);
  * cycle sums of hs_tile_kernel (setup+clear, raster, apply, tiles; zero in normal builds). */
 int hs_get_queue_stats(hs_ctx *ctx, int64_t out[8], int reset_stamps);
 /* Device cell storage (for zero-copy consumers): per stream `stream_words` 4-byte words; each level
- * is a grid of 64 x 32-cell tiles, each tile 16 KB = 2048 log-odds floats followed by 2048 int32
- * updateIndex values; inside a tile's plane the cells are stored in 4 x 4-cell blocks, the blocks
- * row-major (word of cell (lx, ly) = ((ly/4)*16 + lx/4)*16 + (ly%4)*4 + lx%4; DESIGN.md "Data layout"). */
+ * is a grid of 64 x 32-cell tiles, each tile 20 KB = 2048 log-odds floats, then 2048 uint16 update
+ * ordinals h, then 2048 int32 updateIndex values; inside a tile's plane the cells are stored in 4 x 4-cell
+ * blocks, the blocks row-major (element of cell (lx, ly) = ((ly/4)*16 + lx/4)*16 + (ly%4)*4 + lx%4).  A cell's
+ * updateIndex is 3*(E + (h-1)/2) + 1 + (h-1)%2 when h != 0 (E: the stream's ordinal epoch, advanced by the
+ * library's periodic ordinal sweep), else the int32 plane's value; hs_get_map decodes it (DESIGN.md "Data
+ * layout"). */
 int hs_get_device_buffers(hs_ctx *ctx, void **cells, size_t *cells_bytes, size_t *stream_words);
 /* Optional device pose log: every step appends the scan-match pose (float3) of streams [0, streams)
  * at row = steps since hs_reset, i.e. d_buf[(row*streams + s)*3]; rows >= capacity are dropped.

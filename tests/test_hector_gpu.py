@@ -80,6 +80,20 @@ def test_out_of_map_beams_small_map(gpu, scans):
     _run_pair(1, 256, scans, n_scans=15, thresholds=(-1.0, -1.0))
 
 
+@pytest.mark.parametrize("kernel", ["clip", "ring", "binned"])
+@pytest.mark.parametrize("sweep,thresholds", [("1", (-1.0, -1.0)), ("3", (-1.0, -1.0)), ("2", (0.4, 0.9))])
+def test_ordinal_sweep_bitexact(gpu, scans, monkeypatch, kernel, sweep, thresholds):
+    """The updateIndex as a 16-bit hot ordinal + the cold int plane (hector_internal.h ORD_OFF): with an ordinal
+    sweep every 1 / 2 / 3 steps (SLAM2D_ORD_SWEEP; the library's default is 32000), forced updates and the node's
+    gate, every update kernel: every cell's updateIndex (decoded by hs_get_map) and log-odds stay bit-exact."""
+    monkeypatch.setenv("SLAM2D_ORD_SWEEP", sweep)
+    if kernel == "ring":
+        monkeypatch.setenv("SLAM2D_UPD_KERNEL", "ring")
+    elif kernel == "binned":
+        monkeypatch.setenv("SLAM2D_UPDATE", "binned")
+    _run_pair(2, 512, scans, n_scans=12, thresholds=thresholds, stream=3)
+
+
 @pytest.mark.parametrize("cap_env", ["SLAM2D_SEG_CAP", "SLAM2D_ITEM_CAP"])
 def test_unbinned_fallback_bitexact(gpu, scans, monkeypatch, cap_env):
     """Binned path, queue overflow -> WHOLE items (every ray against every tile of the level's bbox)."""

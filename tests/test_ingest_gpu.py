@@ -282,20 +282,26 @@ def test_update_split_knob_same_maps(gpu, monkeypatch):
     fb.close()
 
 
-@pytest.mark.parametrize("S,gate,pipeline", [(7, (-1.0, -1.0), "1"), (6, (0.4, 0.9), "1"), (1, (-1.0, -1.0), "1"),
-                                             (5, (0.4, 0.9), "0")])
-def test_run_ranges_equals_per_step(gpu, monkeypatch, S, gate, pipeline):
+@pytest.mark.parametrize("S,gate,pipeline,sweep", [(7, (-1.0, -1.0), "1", ""), (6, (0.4, 0.9), "1", ""),
+                                                   (1, (-1.0, -1.0), "1", ""), (5, (0.4, 0.9), "0", ""),
+                                                   (7, (-1.0, -1.0), "1", "3"), (5, (-1.0, -1.0), "0", "2")])
+def test_run_ranges_equals_per_step(gpu, monkeypatch, S, gate, pipeline, sweep):
     """hs_run_ranges_device (K steps in one call; SLAM2D_PIPELINE=1: two fleet halves on two HIP streams,
     the grid update of one half beside the other half's match) == K calls of
     hs_step_ranges_batch_device, every pose, gate, map cell and pose-log entry bit for bit; odd fleets
-    split unevenly, S = 1 runs unsplit.  Stream S-1 is also replayed on the oracle."""
+    split unevenly, S = 1 runs unsplit.  Stream S-1 is also replayed on the oracle.  sweep: the run's ordinal
+    sweep every few steps (SLAM2D_ORD_SWEEP; inside the two-half pipeline too) against the per-step fleet's
+    default, so the decoded updateIndex of every cell is compared across the two representations."""
     import torch
     T, LV, SIZE = 8, 2, 384
     scans = synth.make_streams(S, T, with_points=False, seed=77)
     L = _roll_pi_laser()
     monkeypatch.setenv("SLAM2D_PIPELINE", pipeline)
+    if sweep:
+        monkeypatch.setenv("SLAM2D_ORD_SWEEP", sweep)
     fa = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
     monkeypatch.delenv("SLAM2D_PIPELINE")
+    monkeypatch.delenv("SLAM2D_ORD_SWEEP", raising=False)
     fb = HectorFleet(S, 0.05, SIZE, (0.5, 0.5), LV, max_points=N)
     logs = []
     for f in (fa, fb):

@@ -43,9 +43,8 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
   noload     WRONG RESULTS  hs_update_kernel applies its marks to zeros instead of loading the marked quads (prices the
                             apply's load latency, exposed once per tile when the raster before it is short)
   nostore    WRONG RESULTS  hs_update_kernel computes the apply but stores nothing (prices the write traffic)
-  noidx      WRONG RESULTS  hs_update_kernel stores no updateIndex (log-odds exact: prices the index plane's stores)
-  idx16      WRONG RESULTS  hs_update_kernel stores the updateIndex as 16-bit values in the first half of the index plane
-                            (log-odds exact: prices a 16-bit scan-ordinal plane's stores)
+  noord      WRONG RESULTS  hs_update_kernel stores no update ordinal (log-odds exact: prices the ordinal plane's stores;
+                            round 5's noidx / idx16 priced the 32-bit plane before it: profiles/r05/INDEX.md)
   mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
                             streams per CU)
 """
@@ -110,18 +109,7 @@ PATCHES = {
                  "__device__ __forceinline__ void upd_store(int4 *p, int4 v)\n{\n    if (v.x == 1234) *p = v;\n    return;\n#if S2D_NT_STORE"),
                 (K, "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n#if S2D_NT_STORE",
                  "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n    if (v == 1234) *p = v;\n    return;\n#if S2D_NT_STORE")],
-    "noidx": [(K, "                if (qb_all(mb)) {\n                    upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) upd_store(&tu[o + (unsigned)c], uv[c]);\n                }\n", "")],
-    "idx16": [(K, "                if (qb_all(mb)) {\n                    upd_store(reinterpret_cast<int4 *>(&tu[o]), make_int4(uv[0], uv[1], uv[2], uv[3]));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) upd_store(&tu[o + (unsigned)c], uv[c]);\n                }\n",
-               "                {\n"
-               "                    unsigned short *tu16 = reinterpret_cast<unsigned short *>(tu);\n"
-               "                    if (qb_all(mb)) {\n"
-               "                        *reinterpret_cast<uint2 *>(&tu16[o]) = make_uint2((unsigned)(uv[0] & 0xFFFF) | ((unsigned)uv[1] << 16), (unsigned)(uv[2] & 0xFFFF) | ((unsigned)uv[3] << 16));\n"
-               "                    } else {\n"
-               "#pragma unroll\n"
-               "                        for (int c = 0; c < 4; ++c)\n"
-               "                            if (qb_cell(mb, c)) tu16[o + (unsigned)c] = (unsigned short)uv[c];\n"
-               "                    }\n"
-               "                }\n")],
+    "noord": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

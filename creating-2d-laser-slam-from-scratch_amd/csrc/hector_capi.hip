@@ -1191,6 +1191,21 @@ int hs_get_queue_stats(hs_ctx *c, int64_t out[8], int reset_stamps)
     return HS_OK;
 }
 
+int hs_get_diag_stamps(hs_ctx *c, int64_t out[8], int reset)
+{
+    if (!c || !out) return fail(HS_EINVAL, "bad arguments");
+    LOCK(c);
+    unsigned long long st[8];
+    HCHK(hipDeviceSynchronize());
+    HCHK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
+    for (int k = 0; k < 8; ++k) out[k] = (int64_t)st[k];
+    if (reset) {
+        memset(st, 0, sizeof(st));
+        HCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), st, sizeof(st)));
+    }
+    return HS_OK;
+}
+
 int hs_get_device_buffers(hs_ctx *c, void **cells, size_t *cells_bytes, size_t *stream_words)
 {
     if (!c) return fail(HS_EINVAL, "ctx is NULL");

@@ -2227,12 +2227,14 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     // tile is now a ballot, and the extra state cost the kernel two spilled VGPRs.)
     float4 ql[UPD_QUADS];      // pending tile: log-odds of the marked quads (loads in flight)
     unsigned qb[UPD_QUADS];    // pending tile: 12 mark bits per quad (see apply_cell)
+
     float *pend_tl = nullptr;  // pending tile's storage block (null: nothing pending)
     // tile t = part + i * parts of the box (row-major): its column and row are carried from tile to tile
     // (a division of t by the box width per tile was ~20 scalar instructions of signed-division code)
     int tcol = part % ntx, trow = part / ntx;
     for (int ii = 0; ii <= my_tiles; ++ii) {
         const int i = __builtin_amdgcn_readfirstlane(ii);  // uniform (the compiler had put it in a VGPR)
+        const int qtid = tid;  // (the quads' offsets derive from it)
         const int ty = ty0 + trow, tx = tx0 + tcol;
         tcol += parts;
         while (tcol >= ntx) {
@@ -2389,7 +2391,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             for (int j = 0; j < UPD_QUADS; ++j) {
                 const unsigned mb = qb[j];
                 if (!qb_any(mb)) continue;
-                const int qi = tid + j * UPD_THREADS;
+                const int qi = qtid + j * UPD_THREADS;
                 const unsigned o = (unsigned)upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
@@ -2441,7 +2443,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 pend_tl = lvw + (size_t)(tx + ty * (UPD_TH / TILE_H) * g.tiles_x) * TILE_BLOCK_WORDS;
 #pragma unroll
                 for (int j = 0; j < UPD_QUADS; ++j) {
-                    const unsigned qi = (unsigned)tid + j * UPD_THREADS;
+                    const unsigned qi = (unsigned)qtid + j * UPD_THREADS;
                     const int row = (int)(qi >> 4), c4 = (int)((qi & 15u) << 2);
                     const int mw = lds_row(row) + c4;
                     const uint4 m = *reinterpret_cast<const uint4 *>(&marks[mw]);

@@ -34,7 +34,8 @@ def build(force: bool = False) -> str:
 def _declare(L):
     P = C.POINTER
     L.hs_version.restype = C.c_char_p
-    L.hs_source_id.restype = C.c_char_p
+    if hasattr(L, "hs_source_id"):
+        L.hs_source_id.restype = C.c_char_p
     L.hs_last_error.restype = C.c_char_p
     L.hs_create.argtypes = [P(_p), _i, _f, _i, _i, _f, _f, _i, _i]
     L.hs_destroy.argtypes = [_p]
@@ -54,6 +55,8 @@ def _declare(L):
     L.hs_get_poses.argtypes = [_p, _p, _p, _p, _p]
     L.hs_get_counters.argtypes = [_p, _p, _i]
     L.hs_get_queue_stats.argtypes = [_p, _p, _i]
+    if hasattr(L, "hs_get_diag_stamps"):  # (A/B runs may load libraries built before this diagnostic existed)
+        L.hs_get_diag_stamps.argtypes = [_p, _p, _i]
     L.hs_get_device_buffers.argtypes = [_p, P(_p), P(C.c_size_t), P(C.c_size_t)]
     L.hs_set_pose_log.argtypes = [_p, _p, _i, _i]
     L.hs_set_pose_log_slots.argtypes = [_p, _p, _p, _i, _i]
@@ -129,8 +132,9 @@ def source_id_of_tree() -> str:
 
 
 def source_id_of_library() -> str:
-    """The source hash compiled into the loaded library (hs_source_id)."""
-    return lib().hs_source_id().decode()
+    """The source hash compiled into the loaded library (hs_source_id; "" for a library built before it)."""
+    L = lib()
+    return L.hs_source_id().decode() if hasattr(L, "hs_source_id") else ""
 
 
 def check_library_matches_tree() -> str:

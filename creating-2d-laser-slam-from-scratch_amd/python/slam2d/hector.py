@@ -290,6 +290,12 @@ class HectorFleet:
         return {"items": int(o[0]), "segments": int(o[1]), "whole": int(o[2]), "overflow": int(o[3]),
                 "cyc_setup": int(o[4]), "cyc_raster": int(o[5]), "cyc_apply": int(o[6]), "tiles": int(o[7])}
 
+    def diag_stamps(self, reset=True):
+        """hs_get_diag_stamps: the 8 cycle sums a diagnostic build accumulates (tools/build_diag.py)."""
+        o = np.zeros(8, np.int64)
+        check(self.L.hs_get_diag_stamps(self.h, _fp(o), 1 if reset else 0), "hs_get_diag_stamps")
+        return o
+
     def stream_handle(self) -> int:
         return int(self.L.hs_get_stream(self.h) or 0)
 

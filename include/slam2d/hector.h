@@ -172,6 +172,9 @@ int hs_get_counters(hs_ctx *ctx, int64_t out[6], int reset);
  * (unbinned) level items, out[3] overflow events (cumulative); out[4..7] diagnostic-build phase
  * cycle sums of hs_tile_kernel (setup+clear, raster, apply, tiles; zero in normal builds). */
 int hs_get_queue_stats(hs_ctx *ctx, int64_t out[8], int reset_stamps);
+/* The eight diagnostic cycle counters diagnostic builds accumulate (tools/build_diag.py; zero in normal builds:
+ * the product kernels never write them); reset != 0 zeroes them. */
+int hs_get_diag_stamps(hs_ctx *ctx, int64_t out[8], int reset);
 /* Device cell storage (for zero-copy consumers): per stream `stream_words` 4-byte words; each level
  * is a grid of 64 x 32-cell tiles, each tile 20 KB = 2048 log-odds floats, then 2048 uint16 update
  * ordinals h, then 2048 int32 updateIndex values; inside a tile's plane the cells are stored in 4 x 4-cell

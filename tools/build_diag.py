@@ -45,6 +45,10 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
   nostore    WRONG RESULTS  hs_update_kernel computes the apply but stores nothing (prices the write traffic)
   noord      WRONG RESULTS  hs_update_kernel stores no update ordinal (log-odds exact: prices the ordinal plane's stores;
                             round 5's noidx / idx16 priced the 32-bit plane before it: profiles/r05/INDEX.md)
+  ordfull    WRONG RESULTS  hs_update_kernel stores every marked quad's four ordinals in one 8-B store, unmarked cells
+                            included (prices per-cell 2-B stores against one store per quad)
+  uclk       same results   hs_update_kernel's waves sum s_memtime cycles per tile-loop phase (raster, load/store wait,
+                            apply, barrier, mark read) into the diagnostic stamps: tools/clk_update.py reads them
   mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
                             streams per CU)
 """
@@ -110,6 +114,21 @@ PATCHES = {
                 (K, "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n#if S2D_NT_STORE",
                  "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n    if (v == 1234) *p = v;\n    return;\n#if S2D_NT_STORE")],
     "noord": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "")],
+    "ordfull": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n",
+                 "                *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n")],
+    "uclk": [(K, "    for (int ii = 0; ii <= my_tiles; ++ii) {\n        const int i = __builtin_amdgcn_readfirstlane(ii);  // uniform (the compiler had put it in a VGPR)\n        const int qtid = tid;",
+              "    unsigned long long u_r = 0, u_w = 0, u_a = 0, u_b = 0, u_m = 0, u_t = __builtin_amdgcn_s_memtime();\n"
+              "#define UCLK(acc) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); acc += t_ - u_t; u_t = t_; } while (0)\n"
+              "    for (int ii = 0; ii <= my_tiles; ++ii) {\n        UCLK(u_m);\n        const int i = __builtin_amdgcn_readfirstlane(ii);  // uniform (the compiler had put it in a VGPR)\n        const int qtid = tid;"),
+             (K, "        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)\n",
+              "        UCLK(u_r);\n        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)\n        UCLK(u_w);\n"),
+             (K, "            lds_barrier();  // tile i's marks complete\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads",
+              "            UCLK(u_a);\n            lds_barrier();  // tile i's marks complete\n            UCLK(u_b);\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads"),
+             (K, "\n    for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);\n",
+              "\n    UCLK(u_m);\n    if (lane == 0) {\n        atomicAdd(&g_stamps[0], u_r); atomicAdd(&g_stamps[1], u_w); atomicAdd(&g_stamps[2], u_a);\n"
+              "        atomicAdd(&g_stamps[3], u_b); atomicAdd(&g_stamps[4], u_m); atomicAdd(&g_stamps[5], 1ull);\n"
+              "        atomicAdd(&g_stamps[6], (unsigned long long)my_tiles);\n    }\n"
+              "    for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);\n")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

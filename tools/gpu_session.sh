@@ -5,6 +5,8 @@
 #   cold     the driver's exact bench command (python3 bench.py --gpus 1 --steps 20 --warmup 5) -> cold.json
 #            (run it FIRST to time a cold box: no GPU process before it)
 #   pytest   python -m pytest tests -m gpu                                                        -> pytest.log
+#   pytestab:<lib>[:<files>]  the GPU tests against lib/ab/libslam2d_<lib>.so                    -> pytest_<lib>.log
+#   uclk     tools/clk_update.py on lib/ab/libslam2d_uclk.so (the update's tile-loop phase split) -> uclk.json
 #   smoke    __graft_entry__.smoke()                                                              -> smoke.log
 #   warm     the driver's bench command again                                                     -> warm.json
 #   bench:<name>:<args>   bench.py <args> (commas become spaces)                                   -> <name>.json
@@ -26,6 +28,18 @@ for step in "$@"; do
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1 \
         || { echo "FAIL pytest"; tail -30 "$O/pytest.log"; exit 1; }
       tail -2 "$O/pytest.log" ;;
+    pytestab:*)
+      # pytestab:<lib>[:<test files, commas>]  the GPU tests against lib/ab/libslam2d_<lib>.so
+      rest=${step#pytestab:}; lib=${rest%%:*}; files=${rest#*:}; [ "$files" = "$rest" ] && files=tests
+      SLAM2D_LIB=$R/creating-2d-laser-slam-from-scratch_amd/lib/ab/libslam2d_$lib.so timeout -k 10 900 \
+        python3 -u -m pytest ${files//,/ } -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest_$lib.log" 2>&1 \
+        || { echo "FAIL pytestab $lib"; tail -30 "$O/pytest_$lib.log"; exit 1; }
+      echo "pytest $lib: $(tail -1 "$O/pytest_$lib.log")" ;;
+    uclk)
+      # the update kernel's tile-loop phase split (tools/build_diag.py uclk; built beforehand into lib/ab/)
+      SLAM2D_LIB=$R/creating-2d-laser-slam-from-scratch_amd/lib/ab/libslam2d_uclk.so timeout -k 10 300 \
+        python3 tools/clk_update.py > "$O/uclk.json" 2> "$O/uclk.err" || { echo "FAIL uclk"; tail -20 "$O/uclk.err"; exit 1; }
+      cat "$O/uclk.json" ;;
     smoke)
       timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
         || { echo "FAIL smoke"; tail -20 "$O/smoke.log"; exit 1; }

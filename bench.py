@@ -44,6 +44,9 @@ CONFIGS = {
     "c3": dict(map_size=4096, levels=3, streams=1024),  # 1024 x 176 MB pyramids = 180 GB of HBM
 }
 KERNELS = ("match", "bin", "update")
+# the least a once-per-scan update moves per distinct cell it changes: the 4-B log-odds read, the 4-B log-odds
+# written and the 2-B update ordinal written (hector_internal.h ORD_OFF; 12 B with round 4's 4-B updateIndex)
+FLOOR_BYTES_PER_CELL = 10
 PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_traffic.json")  # written by tools/summarize_profile.py
 
 
@@ -311,7 +314,7 @@ def north_star_targets(value, cpu, roof, pose):
     reference CPU path on 1 GPU (against one core, and against all the box's cores used here), >= 40 % of
     the HBM roofline, pose error <= 1e-4 m / rad.
     The roofline rows are counted bytes only: the dominant kernel's counted HBM traffic (rocprofv3 FETCH_SIZE x 2
-    + WRITE_SIZE) and its distinct-cell floor (12 B per distinct cell), each over its launch time.  SURVEY 8d's
+    + WRITE_SIZE) and its distinct-cell floor (10 B per distinct cell), each over its launch time.  SURVEY 8d's
     touch model is not a traffic figure (its rate passes the HBM peak, see roofline.survey_8d_note), so it is
     not a target row.  The north star's "HBM-READ roofline" cannot be met by this workload: the update writes
     every cell it reads, so counted reads are at most ~39 % of its counted traffic and a read fraction >= 0.40
@@ -329,7 +332,7 @@ def north_star_targets(value, cpu, roof, pose):
                                         basis="dominant kernel: counted HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE) per "
                                               "launch / avg launch time / 8 TB/s"),
             "hbm_roofline_distinct_cell_floor": row(roof.get("min_traffic_frac"), 0.40, ">=",
-                                                    basis="update: 12 B per distinct cell / avg launch time / 8 TB/s"),
+                                                    basis="update: 10 B per distinct cell / avg launch time / 8 TB/s"),
             "read_roofline_counted": row(roof.get("read_only_frac_counters"), 0.40, ">=",
                                          basis="rocprofv3 FETCH_SIZE x 2 of the step's kernels / step wall time",
                                          bound=roof.get("read_share_of_counted"),
@@ -992,8 +995,8 @@ def main():
             ksym = kernel_symbol(dom, ktimes)
             pmc, pmc_why = pmc_traffic(ksym, workload, avg_s * 1e9)
             # distinct-cell floor of the update: every cell the scan changes is read once (4 B log-odds)
-            # and written once (4 B log-odds + 4 B updateIndex) -- the least any once-per-scan update moves
-            floor = ctr_i["touched"] * 12 / nlaunch if dom == "update" else ab_i[dom] / nlaunch
+            # and written once (4 B log-odds + 2 B update ordinal) -- the least this layout's update moves
+            floor = ctr_i["touched"] * FLOOR_BYTES_PER_CELL / nlaunch if dom == "update" else ab_i[dom] / nlaunch
             model_8d = ab_i[dom] / nlaunch
             # achieved / frac: counted HBM bytes (PMC summary of this exact workload) when available, else
             # the distinct-cell floor -- both are bytes the kernel really moves, so frac <= 1.  SURVEY 8d's
@@ -1006,7 +1009,7 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
                     "achieved_basis": ("PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) / avg launch time"
-                                       if pmc else "distinct-cell floor (12 B per distinct cell) / avg launch time"),
+                                       if pmc else "distinct-cell floor (10 B per distinct cell) / avg launch time"),
                     "traffic_source": (f"{pmc_why} (FETCH_SIZE x2 + WRITE_SIZE)" if pmc else pmc_why),
                     "min_traffic_per_launch": int(floor) if dom == "update" else None,
                     "min_traffic_frac": (round(floor / avg_s / 1e9 / HBM_PEAK_GBS, 5) if dom == "update" else None),

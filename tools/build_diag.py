@@ -49,6 +49,8 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
                             included (prices per-cell 2-B stores against one store per quad)
   uclk       same results   hs_update_kernel's waves sum s_memtime cycles per tile-loop phase (raster, load/store wait,
                             apply, barrier, mark read) into the diagnostic stamps: tools/clk_update.py reads them
+  nobar      WRONG RESULTS  hs_update_kernel without the per-tile barrier (each wave reads its quads' marks when its own
+                            raster is done; races with the other waves' rasters): prices the four waves' coupling
   mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
                             streams per CU)
 """
@@ -129,6 +131,8 @@ PATCHES = {
               "        atomicAdd(&g_stamps[3], u_b); atomicAdd(&g_stamps[4], u_m); atomicAdd(&g_stamps[5], 1ull);\n"
               "        atomicAdd(&g_stamps[6], (unsigned long long)my_tiles);\n    }\n"
               "    for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);\n")],
+    "nobar": [(K, "            lds_barrier();  // tile i's marks complete\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads",
+               "            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: no barrier\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

@@ -51,6 +51,9 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
                             apply, barrier, mark read) into the diagnostic stamps: tools/clk_update.py reads them
   nobar      WRONG RESULTS  hs_update_kernel without the per-tile barrier (each wave reads its quads' marks when its own
                             raster is done; races with the other waves' rasters): prices the four waves' coupling
+  mclk       same results   hs_match_kernel's chain wave sums s_memtime cycles per Gauss-Newton step: step start -> chain
+                            start (gathers, conversions, chunk 0), the chain, its end -> the next step (solve, broadcast);
+                            tools/clk_match.py reads them
   mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
                             streams per CU)
 """
@@ -133,6 +136,20 @@ PATCHES = {
               "    for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);\n")],
     "nobar": [(K, "            lds_barrier();  // tile i's marks complete\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads",
                "            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: no barrier\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads")],
+    "mclk": [(K, "template <int NP>\n__device__ __forceinline__ void gn_step_cw(",
+              "extern __device__ unsigned long long g_stamps[8];\ntemplate <int NP>\n__device__ __forceinline__ void gn_step_cw("),
+             (K, "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds",
+              "    unsigned long long mk_t0 = __builtin_amdgcn_s_memtime(), mk_t1 = 0, mk_t2 = 0;\n"
+              "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds"),
+             (K, "            lds_barrier();\n            if (lane < 9)\n                run = seq_chain_t<CW_STRIDE>(",
+              "            lds_barrier();\n            if (j == 0) mk_t1 = __builtin_amdgcn_s_memtime();\n            if (lane < 9)\n                run = seq_chain_t<CW_STRIDE>("),
+             (K, "                                             run);\n        }\n    }\n    float *sp = s_pose[parity];\n    if (wave == cw) {\n        float s[9];",
+              "                                             run);\n        }\n        mk_t2 = __builtin_amdgcn_s_memtime();\n    }\n    float *sp = s_pose[parity];\n    if (wave == cw) {\n        float s[9];"),
+             (K, "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS",
+              "    __syncthreads();\n    if (wave == cw && lane == 0) {\n        const unsigned long long mk_t3 = __builtin_amdgcn_s_memtime();\n"
+              "        atomicAdd(&g_stamps[0], mk_t1 - mk_t0); atomicAdd(&g_stamps[1], mk_t2 - mk_t1);\n"
+              "        atomicAdd(&g_stamps[2], mk_t3 - mk_t2); atomicAdd(&g_stamps[3], 1ull);\n    }\n"
+              "    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

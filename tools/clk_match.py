@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase split of hs_match_kernel's reference-order Gauss-Newton step, measured by the `mclk` diagnostic
-build (tools/build_diag.py mclk): the chain wave's clock64() cycles per phase, summed over all streams of K
-steps.  W warm-up steps build the maps with forced updates, then the map-update gate is set out of reach,
+build (tools/build_diag.py mclk): the chain wave's s_memtime cycles per phase (step start -> chain start,
+the chain, chain end -> next step), summed over all streams of K steps (hs_get_diag_stamps).  W warm-up steps build the maps with forced updates, then the map-update gate is set out of reach,
 so the timed steps run the match only (the update kernel exits at once and leaves the counters alone).
 GPU only:  SLAM2D_LIB=.../libslam2d_mclk.so python tools/clk_match.py"""
 import os
@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from slam2d import synth  # noqa: E402
 from slam2d.hector import HectorFleet, HsLaser  # noqa: E402
 
-B, T, W = int(os.environ.get("CLK_STREAMS", 2048)), 8, 4
+B, T, W = int(os.environ.get("CLK_STREAMS", 3840)), 8, 4
 S = synth.make_streams(B, T, seed=12345)
 d_rng = torch.from_numpy(np.ascontiguousarray(S.ranges.transpose(1, 0, 2))).cuda()
 nb = S.ranges.shape[2]
@@ -29,20 +29,16 @@ hs = torch.cuda.current_stream().cuda_stream
 fleet.run_ranges_device(W, d_rng[0].data_ptr(), nb, B * nb, hip_stream=hs)
 torch.cuda.synchronize()
 fleet.set_thresholds(1e9, 1e9)
-fleet.counters(reset=True)
+fleet.diag_stamps(reset=True)
 t0 = time.perf_counter()
 fleet.run_ranges_device(T - W, d_rng[W].data_ptr(), nb, B * nb, hip_stream=hs)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
-c = fleet.counters(reset=True)
-steps = B * (T - W) * 14  # Gauss-Newton steps (6 + 4 + 4 per scan)
-print(f"{T - W} match-only steps of {B} streams in {dt * 1e3:.2f} ms ({dt * 1e3 / (T - W):.3f} ms per step)")
-wg = B * (T - W)
-print(f"per workgroup: ingest prologue {c['cells'] / wg:.0f} cycles, level loop {c['updates'] / wg:.0f} cycles "
-      f"(GN steps {(c['gn_points'] + c['touched'] + c['rays']) / wg:.0f})")
-ph = {"prep (transform, gathers, misses)": c["gn_points"], "chunk loop (chain wave)": c["touched"],
-      "  of which inside seq_chain": c["steps"], "tail + barrier": c["rays"]}
-for k, v in ph.items():
-    print(f"{k:34s} {v / steps:9.0f} cycles per GN step")
-print(f"chain cycles per term (1081 points): {c['steps'] / steps / 1081:.2f}")
+st = fleet.diag_stamps(reset=True)
+n = max(int(st[3]), 1)  # Gauss-Newton steps timed (chain waves)
+print(f"{T - W} match-only steps of {B} streams in {dt * 1e3:.2f} ms ({dt * 1e3 / (T - W):.3f} ms per step); {n} GN steps")
+for name, v in (("pre-chain (transform, gathers, conversions, chunk 0)", st[0]), ("chain (1081 adds x 9 lanes)", st[1]),
+                ("tail (solve, broadcast, barrier)", st[2])):
+    print(f"{name:55s} {v / n:9.0f} cycles per GN step")
+print(f"chain cycles per term: {st[1] / n / 1081:.2f}")
 fleet.close()

@@ -7,6 +7,7 @@
 #   pytest   python -m pytest tests -m gpu                                                        -> pytest.log
 #   pytestab:<lib>[:<files>]  the GPU tests against lib/ab/libslam2d_<lib>.so                    -> pytest_<lib>.log
 #   uclk     tools/clk_update.py on lib/ab/libslam2d_uclk.so (the update's tile-loop phase split) -> uclk.json
+#   mclk     tools/clk_match.py on lib/ab/libslam2d_mclk.so (the match's GN-step phase split)          -> mclk.txt
 #   smoke    __graft_entry__.smoke()                                                              -> smoke.log
 #   warm     the driver's bench command again                                                     -> warm.json
 #   bench:<name>:<args>   bench.py <args> (commas become spaces)                                   -> <name>.json
@@ -40,6 +41,11 @@ for step in "$@"; do
       SLAM2D_LIB=$R/creating-2d-laser-slam-from-scratch_amd/lib/ab/libslam2d_uclk.so timeout -k 10 300 \
         python3 tools/clk_update.py > "$O/uclk.json" 2> "$O/uclk.err" || { echo "FAIL uclk"; tail -20 "$O/uclk.err"; exit 1; }
       cat "$O/uclk.json" ;;
+    mclk)
+      # the match's Gauss-Newton step phase split (tools/build_diag.py mclk; built beforehand into lib/ab/)
+      SLAM2D_LIB=$R/creating-2d-laser-slam-from-scratch_amd/lib/ab/libslam2d_mclk.so timeout -k 10 300 \
+        python3 tools/clk_match.py > "$O/mclk.txt" 2> "$O/mclk.err" || { echo "FAIL mclk"; tail -20 "$O/mclk.err"; exit 1; }
+      cat "$O/mclk.txt" ;;
     smoke)
       timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
         || { echo "FAIL smoke"; tail -20 "$O/smoke.log"; exit 1; }

@@ -137,7 +137,8 @@ PATCHES = {
     "nobar": [(K, "            lds_barrier();  // tile i's marks complete\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads",
                "            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: no barrier\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads")],
     "mclk": [(K, "template <int NP>\n__device__ __forceinline__ void gn_step_cw(",
-              "extern __device__ unsigned long long g_stamps[8];\ntemplate <int NP>\n__device__ __forceinline__ void gn_step_cw("),
+              "extern __device__ unsigned long long g_stamps[8];\n__shared__ unsigned long long s_mk[4];\n"
+              "template <int NP>\n__device__ __forceinline__ void gn_step_cw("),
              (K, "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds",
               "    unsigned long long mk_t0 = __builtin_amdgcn_s_memtime(), mk_t1 = 0, mk_t2 = 0;\n"
               "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds"),
@@ -146,10 +147,13 @@ PATCHES = {
              (K, "                                             run);\n        }\n    }\n    float *sp = s_pose[parity];\n    if (wave == cw) {\n        float s[9];",
               "                                             run);\n        }\n        mk_t2 = __builtin_amdgcn_s_memtime();\n    }\n    float *sp = s_pose[parity];\n    if (wave == cw) {\n        float s[9];"),
              (K, "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS",
-              "    __syncthreads();\n    if (wave == cw && lane == 0) {\n        const unsigned long long mk_t3 = __builtin_amdgcn_s_memtime();\n"
-              "        atomicAdd(&g_stamps[0], mk_t1 - mk_t0); atomicAdd(&g_stamps[1], mk_t2 - mk_t1);\n"
-              "        atomicAdd(&g_stamps[2], mk_t3 - mk_t2); atomicAdd(&g_stamps[3], 1ull);\n    }\n"
-              "    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS")],
+              "    if (wave == cw && lane == 0) {\n        const unsigned long long mk_t3 = __builtin_amdgcn_s_memtime();\n"
+              "        s_mk[0] += mk_t1 - mk_t0; s_mk[1] += mk_t2 - mk_t1; s_mk[2] += mk_t3 - mk_t2; s_mk[3] += 1ull;\n    }\n"
+              "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS"),
+             (K, "    load_exptab();\n    if (!fused) __syncthreads();",
+              "    if (threadIdx.x < 4) s_mk[threadIdx.x] = 0ull;\n    load_exptab();\n    if (!fused) __syncthreads();"),
+             (K, "    clk_stamp(geom.clk, 0, false);\n    if (threadIdx.x != 0) return;",
+              "    clk_stamp(geom.clk, 0, false);\n    if (threadIdx.x == 0) for (int k = 0; k < 4; ++k) atomicAdd(&g_stamps[k], s_mk[k]);\n    if (threadIdx.x != 0) return;")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

@@ -137,10 +137,10 @@ PATCHES = {
     "nobar": [(K, "            lds_barrier();  // tile i's marks complete\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads",
                "            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: no barrier\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads")],
     "mclk": [(K, "template <int NP>\n__device__ __forceinline__ void gn_step_cw(",
-              "extern __device__ unsigned long long g_stamps[8];\n__shared__ unsigned long long s_mk[4];\n"
+              "extern __device__ unsigned long long g_stamps[8];\n__shared__ unsigned long long s_mk[8];\n"
               "template <int NP>\n__device__ __forceinline__ void gn_step_cw("),
              (K, "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds",
-              "    unsigned long long mk_t0 = __builtin_amdgcn_s_memtime(), mk_t1 = 0, mk_t2 = 0;\n"
+              "    unsigned long long mk_t0 = __builtin_amdgcn_s_memtime(), mk_t1 = 0, mk_t2 = 0, mk_pa = 0, mk_pb = 0, mk_pc = 0;\n"
               "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds"),
              (K, "            lds_barrier();\n            if (lane < 9)\n                run = seq_chain_t<CW_STRIDE>(",
               "            lds_barrier();\n            if (j == 0) mk_t1 = __builtin_amdgcn_s_memtime();\n            if (lane < 9)\n                run = seq_chain_t<CW_STRIDE>("),
@@ -149,11 +149,20 @@ PATCHES = {
              (K, "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS",
               "    if (wave == cw && lane == 0) {\n        const unsigned long long mk_t3 = __builtin_amdgcn_s_memtime();\n"
               "        s_mk[0] += mk_t1 - mk_t0; s_mk[1] += mk_t2 - mk_t1; s_mk[2] += mk_t3 - mk_t2; s_mk[3] += 1ull;\n    }\n"
+              "    if (wave != cw && pt == 0) { s_mk[4] += mk_pa - mk_t0; s_mk[5] += mk_pb - mk_pa; s_mk[6] += mk_pc - mk_pb; }\n"
               "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS"),
+             (K, "        if constexpr (CW_SHARE) {\n            if (lane == 0) s_mcnt[pw] = nmiss;",
+              "        mk_pa = __builtin_amdgcn_s_memtime();\n        if constexpr (CW_SHARE) {\n            if (lane == 0) s_mcnt[pw] = nmiss;"),
+             (K, "        lds_barrier();\n    }\n    if (wave != cw) {\n        // chunk j = slot j",
+              "        lds_barrier();\n    }\n    mk_pb = __builtin_amdgcn_s_memtime();\n    if (wave != cw) {\n        // chunk j = slot j"),
+             (K, "            lds_barrier();  // chunk j stored (two buffers: and the chain wave is done with chunk j - 1)\n",
+              "            lds_barrier();  // chunk j stored (two buffers: and the chain wave is done with chunk j - 1)\n            if (j == 0) mk_pc = __builtin_amdgcn_s_memtime();\n"),
+             (K, "        const int c0 = s_mcnt[0], c1 = s_mcnt[1], tot = c0 + c1 + s_mcnt[2];\n",
+              "        const int c0 = s_mcnt[0], c1 = s_mcnt[1], tot = c0 + c1 + s_mcnt[2];\n        if (tid == 0) s_mk[7] += (unsigned long long)tot;\n"),
              (K, "    load_exptab();\n    if (!fused) __syncthreads();",
-              "    if (threadIdx.x < 4) s_mk[threadIdx.x] = 0ull;\n    load_exptab();\n    if (!fused) __syncthreads();"),
+              "    if (threadIdx.x < 8) s_mk[threadIdx.x] = 0ull;\n    load_exptab();\n    if (!fused) __syncthreads();"),
              (K, "    clk_stamp(geom.clk, 0, false);\n    if (threadIdx.x != 0) return;",
-              "    clk_stamp(geom.clk, 0, false);\n    if (threadIdx.x == 0) for (int k = 0; k < 4; ++k) atomicAdd(&g_stamps[k], s_mk[k]);\n    if (threadIdx.x != 0) return;")],
+              "    clk_stamp(geom.clk, 0, false);\n    if (threadIdx.x == 0) for (int k = 0; k < 8; ++k) atomicAdd(&g_stamps[k], s_mk[k]);\n    if (threadIdx.x != 0) return;")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

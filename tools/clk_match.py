@@ -41,4 +41,10 @@ for name, v in (("pre-chain (transform, gathers, conversions, chunk 0)", st[0]),
                 ("tail (solve, broadcast, barrier)", st[2])):
     print(f"{name:55s} {v / n:9.0f} cycles per GN step")
 print(f"chain cycles per term: {st[1] / n / 1081:.2f}")
+# point wave 0, lane 0 (same GN steps): start -> parked (transform + gathers returned + parking stores),
+# parked -> the shared conversion's two barriers passed, -> chunk 0's terms stored and its barrier passed
+for name, v in (("point wave: transform + gathers + parking", st[4]), ("point wave: shared conversion", st[5]),
+                ("point wave: chunk 0 terms", st[6])):
+    print(f"{name:55s} {v / n:9.0f} cycles per GN step")
+print(f"neighbourhood-cache misses (points gathered and converted): {st[7] / n:.1f} per GN step")
 fleet.close()

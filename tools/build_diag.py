@@ -54,6 +54,8 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
   mclk       same results   hs_match_kernel's chain wave sums s_memtime cycles per Gauss-Newton step: step start -> chain
                             start (gathers, conversions, chunk 0), the chain, its end -> the next step (solve, broadcast);
                             tools/clk_match.py reads them
+  cheapprob  WRONG RESULTS  cell_prob is one multiply-add instead of exp + division (prices the match's probability
+                            conversions: their VALU and their place on the per-stream path)
   mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
                             streams per CU)
 """
@@ -140,7 +142,7 @@ PATCHES = {
               "extern __device__ unsigned long long g_stamps[8];\n__shared__ unsigned long long s_mk[8];\n"
               "template <int NP>\n__device__ __forceinline__ void gn_step_cw("),
              (K, "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds",
-              "    unsigned long long mk_t0 = __builtin_amdgcn_s_memtime(), mk_t1 = 0, mk_t2 = 0, mk_pa = 0, mk_pb = 0, mk_pc = 0;\n"
+              "    unsigned long long mk_t0 = __builtin_amdgcn_s_memtime(), mk_t1 = 0, mk_t2 = 0, mk_pa = 0, mk_pb = 0, mk_pc = 0; bool mk_big = false;\n"
               "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds"),
              (K, "            lds_barrier();\n            if (lane < 9)\n                run = seq_chain_t<CW_STRIDE>(",
               "            lds_barrier();\n            if (j == 0) mk_t1 = __builtin_amdgcn_s_memtime();\n            if (lane < 9)\n                run = seq_chain_t<CW_STRIDE>("),
@@ -148,8 +150,8 @@ PATCHES = {
               "                                             run);\n        }\n        mk_t2 = __builtin_amdgcn_s_memtime();\n    }\n    float *sp = s_pose[parity];\n    if (wave == cw) {\n        float s[9];"),
              (K, "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS",
               "    if (wave == cw && lane == 0) {\n        const unsigned long long mk_t3 = __builtin_amdgcn_s_memtime();\n"
-              "        s_mk[0] += mk_t1 - mk_t0; s_mk[1] += mk_t2 - mk_t1; s_mk[2] += mk_t3 - mk_t2; s_mk[3] += 1ull;\n    }\n"
-              "    if (wave != cw && pt == 0) { s_mk[4] += mk_pa - mk_t0; s_mk[5] += mk_pb - mk_pa; s_mk[6] += mk_pc - mk_pb; }\n"
+              "        s_mk[0] += mk_t1 - mk_t0; s_mk[1] += mk_t2 - mk_t1; s_mk[2] += mk_t3 - mk_t2;\n    }\n"
+              "    if (wave != cw && pt == 0) { s_mk[4] += mk_pa - mk_t0; s_mk[5] += mk_pb - mk_pa; s_mk[6] += mk_pc - mk_pb; if (mk_big) s_mk[7] += mk_pb - mk_pa; }\n"
               "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS"),
              (K, "        if constexpr (CW_SHARE) {\n            if (lane == 0) s_mcnt[pw] = nmiss;",
               "        mk_pa = __builtin_amdgcn_s_memtime();\n        if constexpr (CW_SHARE) {\n            if (lane == 0) s_mcnt[pw] = nmiss;"),
@@ -158,11 +160,13 @@ PATCHES = {
              (K, "            lds_barrier();  // chunk j stored (two buffers: and the chain wave is done with chunk j - 1)\n",
               "            lds_barrier();  // chunk j stored (two buffers: and the chain wave is done with chunk j - 1)\n            if (j == 0) mk_pc = __builtin_amdgcn_s_memtime();\n"),
              (K, "        const int c0 = s_mcnt[0], c1 = s_mcnt[1], tot = c0 + c1 + s_mcnt[2];\n",
-              "        const int c0 = s_mcnt[0], c1 = s_mcnt[1], tot = c0 + c1 + s_mcnt[2];\n        if (tid == 0) s_mk[7] += (unsigned long long)tot;\n"),
+              "        const int c0 = s_mcnt[0], c1 = s_mcnt[1], tot = c0 + c1 + s_mcnt[2];\n        mk_big = tot >= 512;\n        if (tid == 0 && mk_big) s_mk[3] += 1ull;\n"),
              (K, "    load_exptab();\n    if (!fused) __syncthreads();",
               "    if (threadIdx.x < 8) s_mk[threadIdx.x] = 0ull;\n    load_exptab();\n    if (!fused) __syncthreads();"),
              (K, "    clk_stamp(geom.clk, 0, false);\n    if (threadIdx.x != 0) return;",
               "    clk_stamp(geom.clk, 0, false);\n    if (threadIdx.x == 0) for (int k = 0; k < 8; ++k) atomicAdd(&g_stamps[k], s_mk[k]);\n    if (threadIdx.x != 0) return;")],
+    "cheapprob": [(K, "    float odds = sdm_expf_tab(l, s_exptab);\n    return __fdiv_rn(odds, odds + 1.0f);",
+                   "    return l * 0.25f + 0.5f;")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
 

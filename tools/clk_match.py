@@ -35,7 +35,8 @@ fleet.run_ranges_device(T - W, d_rng[W].data_ptr(), nb, B * nb, hip_stream=hs)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 st = fleet.diag_stamps(reset=True)
-n = max(int(st[3]), 1)  # Gauss-Newton steps timed (chain waves)
+n = B * 14 * (T - W)  # Gauss-Newton steps timed (3 levels: 4 + 4 + 6 per match)
+nbig = max(int(st[3]), 1)  # of them with >= 512 neighbourhood misses (a level's first step)
 print(f"{T - W} match-only steps of {B} streams in {dt * 1e3:.2f} ms ({dt * 1e3 / (T - W):.3f} ms per step); {n} GN steps")
 for name, v in (("pre-chain (transform, gathers, conversions, chunk 0)", st[0]), ("chain (1081 adds x 9 lanes)", st[1]),
                 ("tail (solve, broadcast, barrier)", st[2])):
@@ -46,5 +47,6 @@ print(f"chain cycles per term: {st[1] / n / 1081:.2f}")
 for name, v in (("point wave: transform + gathers + parking", st[4]), ("point wave: shared conversion", st[5]),
                 ("point wave: chunk 0 terms", st[6])):
     print(f"{name:55s} {v / n:9.0f} cycles per GN step")
-print(f"neighbourhood-cache misses (points gathered and converted): {st[7] / n:.1f} per GN step")
+print(f"steps with >= 512 misses: {nbig} ({nbig / n:.3f} of all); their shared conversion {st[7] / nbig:.0f} cycles, "
+      f"the other steps' {(st[5] - st[7]) / max(n - nbig, 1):.0f}")
 fleet.close()

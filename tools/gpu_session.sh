@@ -12,6 +12,7 @@
 #   warm     the driver's bench command again                                                     -> warm.json
 #   bench:<name>:<args>   bench.py <args> (commas become spaces)                                   -> <name>.json
 #   ab:<lib>,<lib>...     tools/ab_bench.sh over lib/ab/libslam2d_<lib>.so ("main" = the product library)
+#   pmc:<lib>,<lib>...    tools/pmc_ab.sh counter passes per variant (PMC_SETS="set;set" to choose) -> pmc.txt
 #   prof:<name>:<args>    tools/profile_gpu.sh <tag>_<name> <args>
 set -o pipefail
 T=$1; shift
@@ -58,6 +59,11 @@ for step in "$@"; do
     ab:*)
       libs=${step#ab:}
       bash tools/ab_bench.sh "$T" ${libs//,/ } || exit 1 ;;
+    pmc:*)
+      # pmc:<lib>,<lib>...  tools/pmc_ab.sh counters per variant (PMC_SETS from the environment, else its defaults)
+      libs=${step#pmc:}
+      timeout -k 10 900 bash tools/pmc_ab.sh "$T" ${libs//,/ } > "$O/pmc.txt" 2>&1 || { echo "FAIL pmc"; tail -20 "$O/pmc.txt"; exit 1; }
+      cat "$O/pmc.txt" ;;
     prof:*)
       rest=${step#prof:}; name=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
       bash tools/profile_gpu.sh "${T}_$name" ${args//,/ } || { echo "FAIL $step"; exit 1; } ;;

@@ -1,19 +1,19 @@
 #!/bin/bash
-# PMC A/B of library variants over bench.py: tools/pmc_ab.sh <tag> <variant>...  (variant name -> lib/libslam2d_<name>.so, "main")
+# PMC A/B of library variants over bench.py: tools/pmc_ab.sh <tag> <variant>...  (variant name -> lib/ab/libslam2d_<name>.so, "main")
 TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 export TMPDIR=/tmp
 cd /tmp
 for spec in "$@"; do
   v=${spec%%+*}; envs=""; [ "$spec" != "$v" ] && envs=${spec#*+}
-  if [ "$v" = main ]; then lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/libslam2d.so; else lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/libslam2d_$v.so; fi
+  if [ "$v" = main ]; then lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/libslam2d.so; else lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/ab/libslam2d_$v.so; fi
   [ -f "$lib" ] || { echo "missing $lib"; exit 1; }
   tagv=$(echo "$spec" | tr '+=' '__')
   OUT=$ROOT/gpurun_out/pmcab_${TAG}_$tagv; mkdir -p "$OUT"
   i=0
-  for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
-             "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" \
-             "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_ADDR_CONFLICT"; do
+  # PMC_SETS="set;set;..." overrides the default three passes (each set within one pass's block limits)
+  IFS=';' read -r -a SETS <<< "${PMC_SETS:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY;SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_ADDR_CONFLICT}"
+  for set in "${SETS[@]}"; do
     i=$((i+1))
     env SLAM2D_LIB=$lib $envs timeout -k 10 120 rocprofv3 --pmc $set -d "$OUT/p$i" -o run --output-format csv -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-copy-probe --steps 5 --warmup 2 > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   done

@@ -815,6 +815,17 @@ constexpr bool CW_SHARE = S2D_CW_SHARECONV && CW_BUFS == 1;
 #define S2D_PROLOGUE_PRIO 1  // the kernel's prologue and every level's start at that priority too (0: A/B)
 #endif
 
+// cell_word for a cell inside the level (x, y < 2^15) in unsigned 32-bit arithmetic: shifts, masks and one
+// 24-bit multiply (the tile index < 2^13 times the block words), no 64-bit address math.  The match's gathers
+// index the level's uniform base with 4 x this: as 64-bit VGPR addresses (cell_word) they needed 64-bit
+// temporaries, and the compiler's reuse of a slot's load registers for those put a vmcnt(0) between slots
+// 3 and 4 of the gather loop -- two memory round trips per Gauss-Newton step instead of one.
+__device__ __forceinline__ unsigned cell_off(const LevelGeom &g, unsigned x, unsigned y)
+{
+    return __umul24((y / TILE_H) * (unsigned)g.tiles_x + x / TILE, (unsigned)TILE_BLOCK_WORDS) +
+           (unsigned)tile_cell((int)(x % TILE), (int)(y % TILE_H));
+}
+
 template <int NP>
 __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
                                            int n, float f, float *est, float &cs, float &sn, float *H, int parity,
@@ -849,9 +860,12 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
                     key[j] = ((unsigned)iy << 16) | (unsigned)ix;
                     miss[j] = nb_key[slot] != key[j];
                     if (miss[j]) {
+                        // 32-bit byte offsets from the level's (uniform) base: the gathers take the scalar-base +
+                        // VGPR-offset form (cell_off)
                         const unsigned ux = (unsigned)ix, uy = (unsigned)iy;
-                        const float *r0 = cells + cell_word(g, (int)ux, (int)uy);
-                        const float *r1 = cells + cell_word(g, (int)ux, (int)(uy + 1));
+                        const char *cb = reinterpret_cast<const char *>(cells);
+                        const float *r0 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy));
+                        const float *r1 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy + 1u));
                         if ((ux & (CELL_BLK - 1)) != CELL_BLK - 1) {  // (ix, ix + 1) adjacent in a block row
                             float2 a, b;
                             __builtin_memcpy(&a, r0, 8);
@@ -859,9 +873,9 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
                             lg[j][0] = a.x; lg[j][1] = a.y; lg[j][2] = b.x; lg[j][3] = b.y;
                         } else {
                             lg[j][0] = r0[0];
-                            lg[j][1] = cells[cell_word(g, (int)(ux + 1), (int)uy)];
+                            lg[j][1] = *reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy));
                             lg[j][2] = r1[0];
-                            lg[j][3] = cells[cell_word(g, (int)(ux + 1), (int)(uy + 1))];
+                            lg[j][3] = *reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy + 1u));
                         }
                     }
                 }

@@ -1,12 +1,17 @@
 #!/bin/bash
 # A/B library variants in ONE GPU session:  tools/ab_bench.sh <tag> <variant>...
 #   variant = name[+KEY=VAL]  -> lib/ab/libslam2d_<name>.so ("main" = libslam2d.so), optional env KEY=VAL
-# BENCH_ARGS (env) is appended to every bench.py call.
+# BENCH_ARGS (env) is appended to every bench.py call; AB_ROUNDS (env, default 2) rounds.
 TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 mkdir -p "$ROOT/gpurun_out"
-for round in 1 2; do
-  for spec in "$@"; do
+# rounds alternate the order (A B, B A, ...): a lease's clock drifts over a session (the second library of a
+# pair ran 20-40 MHz lower in round 5's A/Bs), so a fixed order biases against the later variants
+SPECS=("$@")
+for round in $(seq 1 "${AB_ROUNDS:-2}"); do
+  ORDER=("${SPECS[@]}")
+  if [ $((round % 2)) -eq 0 ]; then ORDER=(); for ((k=${#SPECS[@]}-1; k>=0; k--)); do ORDER+=("${SPECS[$k]}"); done; fi
+  for spec in "${ORDER[@]}"; do
     v=${spec%%+*}; envs=""; [ "$spec" != "$v" ] && envs=${spec#*+}
     if [ "$v" = main ]; then lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/libslam2d.so; else lib=$ROOT/creating-2d-laser-slam-from-scratch_amd/lib/ab/libslam2d_$v.so; fi
     tagv=$(echo "$spec" | tr '+=' '__')

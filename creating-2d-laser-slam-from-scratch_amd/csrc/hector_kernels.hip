@@ -845,39 +845,43 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
         float lg[NP][4];
         unsigned key[NP];
         bool miss[NP];
+        // every slot's key and its cached key first (the LDS reads in flight together), then the gathers of the
+        // moved points: one LDS latency before the first gather instead of one per slot
+        // (branch-free: a divergent branch here made the compiler wait for each LDS read before the next slot)
+        unsigned kv[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) kv[j] = nb_key[pt + j * CW_PTS];  // (every slot < CW_MAXN has a word)
+        const float lim0 = g.lim[0], lim1 = g.lim[1];
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
             const int slot = pt + j * CW_PTS;
-            miss[j] = false;
-            key[j] = NB_NONE;
-            if (slot < n) {
-                const float px = p[j].x * f, py = p[j].y * f;
-                const float nsn = -sn;
-                const float x = est[0] + (cs * px + nsn * py);
-                const float y = est[1] + (sn * px + cs * py);
-                if ((x >= 0.0f) && (x <= g.lim[0]) && (y >= 0.0f) && (y <= g.lim[1])) {  // NaN -> out of map
-                    const int ix = (int)x, iy = (int)y;
-                    key[j] = ((unsigned)iy << 16) | (unsigned)ix;
-                    miss[j] = nb_key[slot] != key[j];
-                    if (miss[j]) {
-                        // 32-bit byte offsets from the level's (uniform) base: the gathers take the scalar-base +
-                        // VGPR-offset form (cell_off)
-                        const unsigned ux = (unsigned)ix, uy = (unsigned)iy;
-                        const char *cb = reinterpret_cast<const char *>(cells);
-                        const float *r0 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy));
-                        const float *r1 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy + 1u));
-                        if ((ux & (CELL_BLK - 1)) != CELL_BLK - 1) {  // (ix, ix + 1) adjacent in a block row
-                            float2 a, b;
-                            __builtin_memcpy(&a, r0, 8);
-                            __builtin_memcpy(&b, r1, 8);
-                            lg[j][0] = a.x; lg[j][1] = a.y; lg[j][2] = b.x; lg[j][3] = b.y;
-                        } else {
-                            lg[j][0] = r0[0];
-                            lg[j][1] = *reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy));
-                            lg[j][2] = r1[0];
-                            lg[j][3] = *reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy + 1u));
-                        }
-                    }
+            const float px = p[j].x * f, py = p[j].y * f;
+            const float nsn = -sn;
+            const float x = est[0] + (cs * px + nsn * py);
+            const float y = est[1] + (sn * px + cs * py);
+            const bool in = (slot < n) & (x >= 0.0f) & (x <= lim0) & (y >= 0.0f) & (y <= lim1);  // NaN -> out of map
+            key[j] = in ? ((unsigned)(int)y << 16) | (unsigned)(int)x : NB_NONE;  // a slot >= n: no miss
+        }
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            miss[j] = key[j] != NB_NONE && kv[j] != key[j];
+            if (miss[j]) {
+                // 32-bit byte offsets from the level's (uniform) base: the gathers take the scalar-base +
+                // VGPR-offset form (cell_off)
+                const unsigned ux = key[j] & 0xFFFFu, uy = key[j] >> 16;
+                const char *cb = reinterpret_cast<const char *>(cells);
+                const float *r0 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy));
+                const float *r1 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy + 1u));
+                if ((ux & (CELL_BLK - 1)) != CELL_BLK - 1) {  // (ix, ix + 1) adjacent in a block row
+                    float2 a, b;
+                    __builtin_memcpy(&a, r0, 8);
+                    __builtin_memcpy(&b, r1, 8);
+                    lg[j][0] = a.x; lg[j][1] = a.y; lg[j][2] = b.x; lg[j][3] = b.y;
+                } else {
+                    lg[j][0] = r0[0];
+                    lg[j][1] = *reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy));
+                    lg[j][2] = r1[0];
+                    lg[j][3] = *reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy + 1u));
                 }
             }
         }

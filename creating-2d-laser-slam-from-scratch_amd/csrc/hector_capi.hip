@@ -305,16 +305,26 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
     begin_timed(c, 0, s);
     // the register-only instance when no scan of the context can exceed the kernel's register slots
     const MatchIngest mik = mi ? *mi : MatchIngest{};
-#define S2D_MATCH_LAUNCH(SEQ, REGS)                                                                                      \
-    hipLaunchKernelGGL((hs_match_kernel<SEQ, REGS>), dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells,         \
+#define S2D_MATCH_LAUNCH(SEQ, REGS, BIG)                                                                                 \
+    hipLaunchKernelGGL((hs_match_kernel<SEQ, REGS, BIG>), dim3(count), dim3(MATCH_THREADS), 0, s, c->geom, c->d_cells,    \
                        c->d_state, xy, xy_stride, n, origo, hints, begin, mode, out_pose, out_cov, c->plog, wq, wl_cur,   \
                        c->ingest, mik, c->d_ixy, c->max_points)
+    // a level of 2^30 words or more: the gathers' 32-bit byte offsets would overflow (hs_match_kernel BIG)
+    bool big = false;
+    for (int l = 0; l < c->levels; ++l)
+        big = big || (unsigned long long)c->geom.lv[l].tiles_x * c->geom.lv[l].tiles_y * TILE_BLOCK_WORDS >= (1ull << 30);
     if (c->reduce_order == 0) {
-        if (c->max_points <= (S2D_MATCH_CW ? CW_MAXN : MATCH_THREADS * MATCH_REG_PTS)) S2D_MATCH_LAUNCH(true, true);
-        else S2D_MATCH_LAUNCH(true, false);
+        const bool regs = c->max_points <= (S2D_MATCH_CW ? CW_MAXN : MATCH_THREADS * MATCH_REG_PTS);
+        if (big) {
+            if (regs) S2D_MATCH_LAUNCH(true, true, true);
+            else S2D_MATCH_LAUNCH(true, false, true);
+        } else {
+            if (regs) S2D_MATCH_LAUNCH(true, true, false);
+            else S2D_MATCH_LAUNCH(true, false, false);
+        }
     } else {
-        if (c->max_points <= MATCH_THREADS * MATCH_REG_PTS) S2D_MATCH_LAUNCH(false, true);
-        else S2D_MATCH_LAUNCH(false, false);
+        if (c->max_points <= MATCH_THREADS * MATCH_REG_PTS) S2D_MATCH_LAUNCH(false, true, false);
+        else S2D_MATCH_LAUNCH(false, false, false);
     }
 #undef S2D_MATCH_LAUNCH
     end_timed(c, s);

@@ -826,7 +826,7 @@ __device__ __forceinline__ unsigned cell_off(const LevelGeom &g, unsigned x, uns
            (unsigned)tile_cell((int)(x % TILE), (int)(y % TILE_H));
 }
 
-template <int NP>
+template <int NP, bool BIG>
 __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
                                            int n, float f, float *est, float &cs, float &sn, float *H, int parity,
                                            unsigned *nb_key, float4 *nb_val, float (*s_pose)[POSE_WORDS], float *seqT,
@@ -865,7 +865,15 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
             miss[j] = key[j] != NB_NONE && kv[j] != key[j];
-            if (miss[j]) {
+            if (BIG && miss[j]) {
+                // (a level of 2^30 words or more -- maps above ~20000^2 cells, hs_match_kernel<.., .., true>:
+                // 64-bit addresses)
+                const int ux = (int)(key[j] & 0xFFFFu), uy = (int)(key[j] >> 16);
+                lg[j][0] = cells[cell_word(g, ux, uy)];
+                lg[j][1] = cells[cell_word(g, ux + 1, uy)];
+                lg[j][2] = cells[cell_word(g, ux, uy + 1)];
+                lg[j][3] = cells[cell_word(g, ux + 1, uy + 1)];
+            } else if (miss[j]) {
                 // 32-bit byte offsets from the level's (uniform) base: the gathers take the scalar-base +
                 // VGPR-offset form (cell_off)
                 const unsigned ux = key[j] & 0xFFFFu, uy = key[j] >> 16;
@@ -1031,7 +1039,9 @@ constexpr int MATCH_REG_PTS = 5;  // points per thread kept in registers: scans 
 // REGS: every scan of the launch fits the registers (max_points <= CW_MAXN for SEQ, 1280 for the tree
 // order): the HBM-strided Gauss-Newton path is compiled out -- it alone lifted the kernel from 83 to 140
 // VGPRs (SEQ), so the common case no longer pays its register allocation
-template <bool SEQ, bool REGS>
+// BIG: some level holds 2^30 words or more (maps above ~20000^2 cells): the reference-order gathers use 64-bit
+// addresses (cell_word) instead of 32-bit byte offsets from the level base (cell_off)
+template <bool SEQ, bool REGS, bool BIG>
 __global__ void __launch_bounds__(MATCH_THREADS) __attribute__((amdgpu_waves_per_eu(S2D_MATCH_WAVES)))
 hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__restrict__ state,
                 const float2 *__restrict__ xy, int xy_stride, const int *__restrict__ counts,
@@ -1145,7 +1155,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             for (int it = 0; it <= iters; ++it) {
                 if (in_regs) {
                     if constexpr (CW)
-                        gn_step_cw<NPR>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, parity, nb_key, nb_val, s_pose, seqT,
+                        gn_step_cw<NPR, BIG>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, parity, nb_key, nb_val, s_pose, seqT,
                                         cw, pt);
                     else
                         gn_step_reg<NPR, SEQ>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, red, parity, nb_key,

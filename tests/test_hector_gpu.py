@@ -317,6 +317,27 @@ def test_long_rays_over_16384_cells(gpu):
         np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol), err_msg=f"level {lvl}")
 
 
+def test_big_level_gathers_bitexact(gpu, scans):
+    """A level of more than 2^30 storage words (32768 x 13184 cells at level 0: 210944 tiles x 5120 words): the
+    match's gathers would overflow their 32-bit byte offsets from the level base, so the host launches the
+    64-bit-address instance (hs_match_kernel BIG).  Every matched pose, covariance and gate equals the oracle."""
+    sx, sy = 32768, 13184
+    fleet = HectorFleet(1, 0.05, sx, (0.5, 0.5), 2, max_points=1081, map_size_y=sy)
+    ora = O.HectorOracle(0.05, sx, (0.5, 0.5), 2, reduce_threads=T_RED, map_size_y=sy)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(0.4, 0.9)
+    for k in range(8):
+        pts = scans.points[1, k, : scans.counts[1, k]]
+        gp, gc, gd = fleet.update(0, pts, (0.0, 0.0))
+        op, oc, od = ora.process(pts, (0.0, 0.0))
+        assert gd == od, f"scan {k}: did_update {gd} vs {od}"
+        np.testing.assert_array_equal(_bits(gp), _bits(op), err_msg=f"scan {k} pose")
+        np.testing.assert_array_equal(_bits(gc), _bits(oc), err_msg=f"scan {k} cov")
+    fleet.close()
+    ora.close()
+
+
 def test_reset(gpu, scans):
     """HectorSlamProcessor::reset (HectorSlamProcessor.h:111-117): grids cleared and poses reset; the grids'
     update indices (GridMapBase::reset clears cells only), the covariance and the stored containers stay

@@ -56,6 +56,8 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
                             tools/clk_match.py reads them
   cheapprob  WRONG RESULTS  cell_prob is one multiply-add instead of exp + division (prices the match's probability
                             conversions: their VALU and their place on the per-stream path)
+  mlds4      same results   hs_match_kernel with 1.2 KB of unused LDS (5 -> 4 workgroups per CU: is the chain's
+                            contention worth a fifth of the streams per CU?)
   mlds3      same results   hs_match_kernel with 12 KB of unused LDS (4 -> 3 workgroups per CU: prices the match's
                             streams per CU)
 """
@@ -112,6 +114,9 @@ PATCHES = {
     "mlds3": [(K, "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n",
                "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n"
                "    __shared__ float s_pad[3000];\n    if (stream_begin < 0) s_pad[threadIdx.x] = 1.0f;\n")],
+    "mlds4": [(K, "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n",
+               "    __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity\n"
+               "    __shared__ float s_pad[300];\n    if (stream_begin < 0) s_pad[threadIdx.x] = 1.0f;\n")],
     "noload": [(K, "                    if (mk) ql[j] = *reinterpret_cast<const float4 *>(pend_tl + (unsigned)upd_off(row, c4, g.tiles_x));\n",
                 "                    if (mk) ql[j] = make_float4(0.0f, 0.0f, 0.0f, (float)row);\n")],
     "nostore": [(K, "__device__ __forceinline__ void upd_store(float4 *p, float4 v)\n{\n#if S2D_NT_STORE",
@@ -138,9 +143,9 @@ PATCHES = {
               "    for (int off = 32; off >= 1; off >>= 1) touched += __shfl_xor(touched, off, 64);\n")],
     "nobar": [(K, "            lds_barrier();  // tile i's marks complete\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads",
                "            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: no barrier\n            if (s_any[buf] == (unsigned)(i + 1)) {\n                // thread owns quads")],
-    "mclk": [(K, "template <int NP>\n__device__ __forceinline__ void gn_step_cw(",
+    "mclk": [(K, "template <int NP, bool BIG>\n__device__ __forceinline__ void gn_step_cw(",
               "extern __device__ unsigned long long g_stamps[8];\n__shared__ unsigned long long s_mk[8];\n"
-              "template <int NP>\n__device__ __forceinline__ void gn_step_cw("),
+              "template <int NP, bool BIG>\n__device__ __forceinline__ void gn_step_cw("),
              (K, "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds",
               "    unsigned long long mk_t0 = __builtin_amdgcn_s_memtime(), mk_t1 = 0, mk_t2 = 0, mk_pa = 0, mk_pb = 0, mk_pc = 0; bool mk_big = false;\n"
               "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds"),

@@ -6,9 +6,11 @@
  * there:
  *     mapRep = new MapRepHip(mapResolution, mapSizeX, mapSizeY, multi_res_size, startCoords);
  *
- * This header is compiled in the maintainer's ROS workspace, next to the reference headers it includes
- * (they need Eigen3, which this repository's image lacks); every call it makes goes through
- * slam2d::HectorMapBackend (hector_map_backend.hpp), which is compiled and tested here
+ * This header is built in the maintainer's ROS workspace, next to the reference headers it includes (they need
+ * Eigen3, which this repository's image lacks).  Here it is compile-checked against the reference's own headers
+ * with an API-only Eigen stand-in (tests/cpp/maprep_compile_check.cpp, `make -C tests/cpp maprep_check`: every
+ * pure virtual overridden, the members instantiated; spelling and signatures only, nothing run).  Every call it
+ * makes goes through slam2d::HectorMapBackend (hector_map_backend.hpp), which is compiled and tested here
  * (tests/cpp/hector_threads_test.cpp: a spin thread updating while a publish thread refreshes).
  *
  * Behaviour kept from MapRepMultiMap (MapRepMultiMap.h) / MapProcContainer (MapProcContainer.h):
@@ -61,7 +63,9 @@ public:
     }
     ~MapRepHip() override
     {
-        for (MapLockerInterface *m : mutexes_) delete m;  // MapProcContainer::cleanup owns the lockers
+        // MapProcContainer::cleanup owns and deletes the lockers (MapProcContainer.h:65-67) through the interface,
+        // which has no virtual destructor in the reference (MapLockerInterface.h:31-36): the same deletion is kept
+        for (MapLockerInterface *m : mutexes_) delete m;
     }
 
     void reset() override

@@ -140,6 +140,34 @@ def test_backend_header_compiles_as_cpp17():
     assert r.returncode == 0, r.stderr
 
 
+REF_HECTOR = "/root/reference/lesson4/include/lesson4/hector_mapping"
+
+
+def _maprep_compile(extra_src: str = ""):
+    """Compile include/slam2d/MapRepHip.h (+ extra_src) against the reference's Hector headers and the API-only Eigen
+    stand-in tests/cpp/eigen_api_stub (tests/cpp/Makefile maprep_check's flags): spelling and signatures only."""
+    cpp = os.path.join(REPO, "tests", "cpp")
+    src = open(os.path.join(cpp, "maprep_compile_check.cpp")).read() + extra_src
+    return subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-Wno-delete-non-virtual-dtor", "-Wno-unused-function",
+                           "-fsyntax-only", "-I", os.path.join(cpp, "eigen_api_stub"), "-I", os.path.dirname(INC),
+                           "-I", os.path.join(REF_HECTOR, "slam_main"), "-x", "c++", "-"],
+                          input=src, capture_output=True, text=True, cwd=cpp)
+
+
+def test_maprep_hip_compiles_against_reference_headers():
+    """the drop-in MapRepresentationInterface (MapRepresentationInterface.h:44-69, swapped in at
+    HectorSlamProcessor.h:61) is concrete and its members instantiate against the reference's own headers.  A
+    misspelled override must fail the same compile (the check has teeth).  Needs the reference tree (build container)."""
+    if not os.path.exists(os.path.join(REF_HECTOR, "slam_main", "MapRepresentationInterface.h")):
+        pytest.skip("reference headers absent (GPU box)")
+    r = _maprep_compile()
+    assert r.returncode == 0, r.stderr
+    bad = _maprep_compile("struct Slip : hectorslam::MapRepHip {\n"
+                          "  using hectorslam::MapRepHip::MapRepHip;\n"
+                          "  const hectorslam::GridMap &getGridmap(int l) const override { return getGridMap(l); }\n};\n")
+    assert bad.returncode != 0 and "override" in bad.stderr, bad.stderr
+
+
 def test_cpp_test_host_links_the_product_library():
     """tests/cpp/build/hector_threads_test (built by build()) resolves libslam2d.so from the tree."""
     b = os.path.join(REPO, "tests", "cpp", "build", "hector_threads_test")

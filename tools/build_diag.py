@@ -45,6 +45,11 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
   nostore    WRONG RESULTS  hs_update_kernel computes the apply but stores nothing (prices the write traffic)
   noord      WRONG RESULTS  hs_update_kernel stores no update ordinal (log-odds exact: prices the ordinal plane's stores;
                             round 5's noidx / idx16 priced the 32-bit plane before it: profiles/r05/INDEX.md)
+  ordbm      WRONG RESULTS  hs_update_kernel stores, per wave and marked tile, its lanes' mark + hit bits (one 2-B store per
+                            lane, 128 B per wave) and a 16-B header from lane 0 instead of the ordinals (prices a bitmap
+                            log of the ordinal plane, round-6 VERDICT item 1; the fold kernel is priced separately)
+  ordbm2     WRONG RESULTS  ordbm without the header store and the any-mark test: every thread of a tile with marks stores
+                            its 2-B bit word (the floor of a bitmap log's store cost in the update)
   ordfull    WRONG RESULTS  hs_update_kernel stores every marked quad's four ordinals in one 8-B store, unmarked cells
                             included (prices per-cell 2-B stores against one store per quad)
   uclk       same results   hs_update_kernel's waves sum s_memtime cycles per tile-loop phase (raster, load/store wait,
@@ -126,6 +131,22 @@ PATCHES = {
                 (K, "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n#if S2D_NT_STORE",
                  "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n    if (v == 1234) *p = v;\n    return;\n#if S2D_NT_STORE")],
     "noord": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "")],
+    "ordbm": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "                (void)uv;\n"),
+              (K, "                touched += qb_count(mb);\n            }\n            pend_tl = nullptr;\n",
+               "                touched += qb_count(mb);\n            }\n            {\n                unsigned bm = 0u;\n#pragma unroll\n"
+               "                for (int j = 0; j < UPD_QUADS; ++j) {\n                    const unsigned u = ~qb[j] & QB_UNMASK;\n"
+               "                    const unsigned mk = ((u >> 7) & 1u) | ((u >> 14) & 2u) | ((u >> 21) & 4u) | (u >> 28);\n"
+               "                    bm |= (mk | (qb_hits(qb[j]) << 3)) << (8 * j);\n                }\n"
+               "                if (__any(bm != 0u)) {\n                    tu[qtid] = (unsigned short)bm;\n"
+               "                    if (lane == 0) *reinterpret_cast<uint4 *>(&pend_tl[ORD_OFF + 512 + 4 * (qtid >> 6)]) = "
+               "make_uint4(mark_free, (unsigned)(size_t)pend_tl, 0u, 0u);\n                }\n            }\n            pend_tl = nullptr;\n")],
+    "ordbm2": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "                (void)uv;\n"),
+               (K, "                touched += qb_count(mb);\n            }\n            pend_tl = nullptr;\n",
+                "                touched += qb_count(mb);\n            }\n            {\n                unsigned bm = 0u;\n#pragma unroll\n"
+                "                for (int j = 0; j < UPD_QUADS; ++j) {\n                    const unsigned u = ~qb[j] & QB_UNMASK;\n"
+                "                    const unsigned mk = ((u >> 7) & 1u) | ((u >> 14) & 2u) | ((u >> 21) & 4u) | (u >> 28);\n"
+                "                    bm |= (mk | (qb_hits(qb[j]) << 3)) << (8 * j);\n                }\n"
+                "                tu[qtid] = (unsigned short)(bm | (mark_free << 16));\n            }\n            pend_tl = nullptr;\n")],
     "ordfull": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n",
                  "                *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n")],
     "uclk": [(K, "    for (int ii = 0; ii <= my_tiles; ++ii) {\n        const int i = __builtin_amdgcn_readfirstlane(ii);  // uniform (the compiler had put it in a VGPR)\n        const int qtid = tid;",

@@ -67,6 +67,15 @@ for step in "$@"; do
     prof:*)
       rest=${step#prof:}; name=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
       bash tools/profile_gpu.sh "${T}_$name" ${args//,/ } || { echo "FAIL $step"; exit 1; } ;;
+    calib)
+      # WRITE_SIZE / FETCH_SIZE calibration on the update's store shapes (tools/probes/write_calib.hip, built
+      # beforehand into tools/probes/build/): one plain run, then one --pmc pass per counter
+      B=$R/tools/probes/build/write_calib
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 60 "$B" > "$O/expected.json" 2> "$O/calib.err" \
+        && timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$O/write" -o run --output-format csv -- "$B" > "$O/w.log" 2>&1 \
+        && timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$O/fetch" -o run --output-format csv -- "$B" > "$O/f.log" 2>&1) \
+        || { echo "FAIL calib"; tail -20 "$O/calib.err" "$O/w.log" "$O/f.log" 2>/dev/null; exit 1; }
+      python3 tools/write_calib.py "$O" "$O/write_calib" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

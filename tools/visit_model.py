@@ -6,6 +6,14 @@ For a few synthetic scans (python/slam2d/synth.py, 2048^2 x 3 levels at 20 cells
   ray box meets the tile (the wave runs the clip setup); pairs where some lane's walk has a step in the tile
   (useful setups); the cone cull's (S2D_WEDGE) survivors; and the lane occupancy of the setups.
     python3 tools/visit_model.py [scans]
+
+Round 6 adds the per-tile wave balance: each tile's raster is run by the four waves of the
+workgroup, wave w taking the fan groups fi = w, w + 4, ...; a wave's raster cost on a tile is modelled as
+SETUP instructions per (tile, group) clip setup plus STEP per step of the longest walk among the group's lanes
+in that tile.  The barrier after the raster makes the busiest wave the tile's path, so the model prints, per
+level, sum over tiles of the busiest wave's cost / sum of the mean wave's cost, the share of tiles (with steps)
+crossed by <= 2 fan groups, and the same ratio for two alternatives: two-wave workgroups on 64 x 16 tiles
+(groups fi = w, w + 2, ...), whose busiest wave summed over a 64 x 32 area is the last column.
 """
 import os
 import sys
@@ -20,6 +28,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from test_cone_cull_cpu import cone_meets, fan_cone, walk_cells  # noqa: E402
 
 TILE, TILE_H = 64, 32
+SETUP, STEP = 150, 5  # VALU-instruction model of one (tile, group) clip setup and one walk step
 
 
 def level_rays(pts, pose, level, size=2048):
@@ -38,6 +47,7 @@ def main():
     nscans = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     ss = synth.make_streams(nscans, 1, distinct_paths=nscans)
     tot = np.zeros((3, 7))
+    bal = {(lvl, nw): np.zeros(4) for lvl in range(3) for nw in (4, 2)}
     for k in range(nscans):
         pts = ss.points[k, 0, :ss.counts[k, 0]]
         pose = ss.gt[k, 0] * 0  # first scan of each path: pose (0, 0, 0) in its own frame
@@ -78,12 +88,46 @@ def main():
                         if use:
                             useful += 1
             tot[lvl] += [ntiles, ballot, setup, useful, cone_setup, lanes_setup, lanes_useful]
+            # wave balance: per (tile, fan group) the clip setup and the longest walk of its lanes in the tile
+            for th, nw in ((TILE_H, 4), (TILE_H // 2, 2)):
+                cost = {}  # tile -> per-wave cost
+                ngroups = {}
+                for i in range(n):
+                    if not valid[i]:
+                        continue
+                    cx, cy = cells[i]
+                    tx = (cx + x0) // TILE
+                    ty = (cy + y0) // th
+                    # free steps are cells 0..L-1 (the end cell is the hit); count per tile
+                    keys, cnt = np.unique(np.stack([tx[:-1], ty[:-1]], 1), axis=0, return_counts=True) if len(tx) > 1 \
+                        else (np.zeros((0, 2), int), np.zeros(0, int))
+                    fi = i // 64
+                    for (a, b), c in zip(keys.tolist(), cnt.tolist()):
+                        d = cost.setdefault((a, b), {})
+                        d[fi] = max(d.get(fi, 0), c)
+                busy = mean = 0.0
+                few = 0
+                for t, d in cost.items():
+                    w = np.zeros(nw)
+                    for fi, steps in d.items():
+                        w[fi % nw] += SETUP + STEP * steps
+                    busy += w.max()
+                    mean += w.mean()
+                    few += len(d) <= 2
+                bal[(lvl, nw)] += np.array([busy, mean, few, len(cost)])
     print(f"{nscans} scans; per scan and level:")
     print("level  box-tiles  ballot-pairs  setups  useful-setups  setups-after-cone  lanes/setup  useful-lanes/setup")
     for lvl in range(3):
         t = tot[lvl] / nscans
         print(f"{lvl:5d} {t[0]:10.0f} {t[1]:13.0f} {t[2]:7.0f} {t[3]:14.0f} {t[4]:18.0f} {t[5] / max(t[2], 1):12.1f} "
               f"{t[6] / max(t[2], 1):19.1f}")
+    print(f"wave balance (model: {SETUP} per clip setup + {STEP} per walk step; busiest wave / mean wave, summed over tiles):")
+    print("level  4 waves x 64x32: busiest/mean  tiles<=2 groups  raster per tile (busiest)  |  2 waves x 64x16: busiest/mean  "
+          "raster per 64x32 area (busiest)")
+    for lvl in range(3):
+        b4, b2 = bal[(lvl, 4)], bal[(lvl, 2)]
+        print(f"{lvl:5d} {b4[0] / b4[1]:31.2f} {b4[2] / b4[3]:16.2f} {b4[0] / b4[3]:26.0f}  |  {b2[0] / b2[1]:31.2f} "
+              f"{b2[0] / b4[3]:31.0f}")
 
 
 if __name__ == "__main__":

@@ -126,6 +126,28 @@ def pmc_traffic(kernel: str, workload: dict, live_avg_ns: float | None = None):
     return found, found["source"]
 
 
+def write_calibration():
+    """The committed WRITE_SIZE / FETCH_SIZE calibration on the update's store and load shapes
+    (tools/probes/write_calib.hip -> profiles/r06/write_calib.json; MI355X_MICROARCH.md's HBM section leaves the
+    counters uncalibrated for other widths than 16-B stores): per shape the counted bytes over the 32-B sectors
+    written (stores) or over the bytes loaded (2 x FETCH_SIZE).  None when the file is absent."""
+    path = os.path.join(REPO, "profiles", "r06", "write_calib.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ratios = {}
+    for r in d.get("shapes", []):
+        k = r["kernel"].replace("cal_", "")
+        v = r.get("fetch_x2_over_bytes") if k.startswith("ld") else r.get("write_over_sectors32")
+        if v is not None:
+            ratios[k] = round(v, 4)
+    return {"source": "profiles/r06/write_calib.md",
+            "meaning": "stores: WRITE_SIZE / (32-B sectors written x 32 B); loads: 2 x FETCH_SIZE / bytes loaded",
+            "ratios": ratios}
+
+
 def aggregate_over_ranks(elapsed: float, units: float, device):
     """Whole-job timing: the slowest rank's time (MAX) and the units all ranks processed (SUM).
     Works on any backend (RCCL on the GPU box, gloo in the CPU tests)."""
@@ -1027,8 +1049,11 @@ def main():
             roof = {"bound": "hbm", "kernel": ksym, "achieved": round(achieved, 2),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
-                    "achieved_basis": ("PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) / avg launch time"
+                    "achieved_basis": ("PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) / avg launch time; the "
+                                       "counters calibrated on the update's own shapes (traffic_calibration): WRITE_SIZE "
+                                       "is the 32-B sectors written, 2 x FETCH_SIZE the bytes of its 16-B loads"
                                        if pmc else "distinct-cell floor (10 B per distinct cell) / avg launch time"),
+                    "traffic_calibration": write_calibration(),
                     "traffic_source": (f"{pmc_why} (FETCH_SIZE x2 + WRITE_SIZE)" if pmc else pmc_why),
                     "min_traffic_per_launch": int(floor) if dom == "update" else None,
                     "min_traffic_frac": (round(floor / avg_s / 1e9 / HBM_PEAK_GBS, 5) if dom == "update" else None),

@@ -221,6 +221,10 @@ int reset_all(hs_ctx *c, bool full)
             o.pose[0] = o.pose[1] = o.pose[2] = 0.0f;
             o.do_update = 0;
             o.step_index = 0;
+            // the fill zeroed every hot ordinal: a fresh ordinal epoch at the stream's current update (decoding
+            // needs E only for non-zero ordinals), which also clears an ordinal overflow
+            o.ord_epoch = o.cur_update_index / 3;
+            o.ord_overflow = 0;
             h[s] = o;
         }
     }
@@ -229,6 +233,7 @@ int reset_all(hs_ctx *c, bool full)
         for (int i = 0; i < 2; ++i)
             if (c->wl[p][i]) HCHK(hipMemsetAsync(c->wl[p][i], 0, sizeof(int) * 4, c->stream));
     for (int p = 0; p < MAX_PARTS; ++p) c->wl_parity[p] = 0;
+    c->ord_steps = 0;  // every stream starts a new ordinal epoch
     HCHK(hipStreamSynchronize(c->stream));
     return HS_OK;
 }
@@ -414,7 +419,10 @@ int launch_part(hs_ctx *c, int part, int begin, int count, const float2 *xy, int
 // 2 (k - E) + 2 stays below 2^16).  On stream s, after the previous steps and before this one.
 int ord_sweep_if_due(hs_ctx *c, hipStream_t s)
 {
-    if (++c->ord_steps <= c->ord_interval) return HS_OK;
+    if (c->ord_steps < c->ord_interval) {
+        ++c->ord_steps;
+        return HS_OK;
+    }
     const int tiles = (int)(c->geom.cells_words / TILE_BLOCK_WORDS);
     hipLaunchKernelGGL(hs_ord_sweep_kernel, dim3(4096), dim3(256), 0, s, c->d_cells, c->d_state, c->geom.stream_words,
                        tiles, 0, c->B);
@@ -609,10 +617,12 @@ int hs_create(hs_ctx **out, int num_streams, float map_resolution, int map_size_
         c->reduce_order = (mo && strcmp(mo, "tree") == 0) ? MATCH_THREADS : 0;
         const char *fi = getenv("SLAM2D_FUSE_INGEST");
         c->fuse_ingest = !(fi && atoi(fi) == 0);
-        // steps between ordinal sweeps (tests set a few to exercise the sweep; at most ORD_SWEEP_MAX)
+        // steps between ordinal sweeps (tests set a few to exercise the sweep; at most ORD_SWEEP_MAX).  0: never
+        // (TEST ONLY: stands for a caller that replays graph captures of *_device calls without hs_flush_ordinals,
+        // to exercise the device's ordinal-overflow flag)
         if (const char *os = getenv("SLAM2D_ORD_SWEEP")) {
             const int v = atoi(os);
-            c->ord_interval = v < 1 ? 1 : (v > ORD_SWEEP_MAX ? ORD_SWEEP_MAX : v);
+            c->ord_interval = v == 0 ? INT_MAX : (v < 1 ? 1 : (v > ORD_SWEEP_MAX ? ORD_SWEEP_MAX : v));
         }
         const char *np = getenv("SLAM2D_PARTS");
         c->nparts = np ? atoi(np) : 1;
@@ -899,6 +909,10 @@ int hs_get_map(hs_ctx *c, int stream, int level, int8_t *occ_out, float *logodds
     StreamState st;
     HCHK(hipMemcpyAsync(&st, c->d_state + stream, sizeof(st), hipMemcpyDeviceToHost, c->stream));
     HCHK(hipStreamSynchronize(c->stream));
+    if (upd_out && st.ord_overflow)
+        return fail(HS_ESTATE, "stream's update ordinals overflowed 16 bits: more than 32000 map updates without the "
+                               "library's ordinal sweep (replayed graph captures of *_device calls?); call "
+                               "hs_flush_ordinals at least every 32000 steps; hs_reset clears the state");
     if (!tmp.empty()) {
         for (int y = 0; y < L.sy; ++y)
             for (int x = 0; x < L.sx; ++x) {
@@ -1214,6 +1228,19 @@ int hs_get_diag_stamps(hs_ctx *c, int64_t out[8], int reset)
         HCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), st, sizeof(st)));
     }
     return HS_OK;
+}
+
+int hs_flush_ordinals(hs_ctx *c, void *hip_stream)
+{
+    if (!c) return fail(HS_EINVAL, "ctx is NULL");
+    LOCK(c);
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    if (dev_enter(c, s) != HS_OK) return HS_EHIP;
+    c->ord_steps = c->ord_interval;  // due now
+    const int rc = ord_sweep_if_due(c, s);
+    if (rc != HS_OK) return rc;
+    c->ord_steps = 0;  // no step of the new epoch has run yet
+    return dev_leave(c, s);
 }
 
 int hs_get_device_buffers(hs_ctx *c, void **cells, size_t *cells_bytes, size_t *stream_words)

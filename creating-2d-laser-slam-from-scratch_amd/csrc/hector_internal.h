@@ -130,6 +130,10 @@ struct alignas(16) StreamState {
     int step_index;                   // steps since hs_reset (pose-log row)
     int ord_epoch;                    // E: update ordinal of the last ordinal sweep (see ORD_OFF)
     int ord_base;                     // this step's hot ordinal of a freed cell, 2 (k - E) + 1 (+1: occupied)
+    // sticky: an update's hot ordinal passed 0xFFFF, i.e. more than ORD_SWEEP_MAX updates went by without the
+    // library's ordinal sweep (e.g. replayed graph captures of *_device calls): hs_get_map refuses to decode the
+    // stream's updateIndex until hs_reset; the log-odds are unaffected
+    int ord_overflow;
     // MapRepMultiMap::dataContainers (MapRepMultiMap.h:89, :161): the DataContainer of the last
     // matchData, which updateByScan draws into levels >= 1 (:187).  Its points (level-0 scale) live in
     // the context's per-stream container buffer; empty (mc_n = 0) until the first match.

@@ -1249,6 +1249,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
         // the hot ordinal of this update k = currUpdateIndex / 3 (hector_internal.h ORD_OFF): freed cells get
         // 2 (k - E) + 1, occupied ones + 1
         st.ord_base = 2 * (st.cur_update_index / 3 - st.ord_epoch) + 1;
+        if (st.ord_base >= 0xFFFF) st.ord_overflow = 1;  // its occupied ordinal would not fit 16 bits (no sweep)
         st.cur_update_index += 3;            // OccGridMapBase.h:167
         st.map_updates += 1;                 // GridMapBase::setUpdated (GridMapBase.h:333)
         st.step_cells = 0;

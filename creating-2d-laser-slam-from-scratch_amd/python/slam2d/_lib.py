@@ -58,6 +58,8 @@ def _declare(L):
     if hasattr(L, "hs_get_diag_stamps"):  # (A/B runs may load libraries built before this diagnostic existed)
         L.hs_get_diag_stamps.argtypes = [_p, _p, _i]
     L.hs_get_device_buffers.argtypes = [_p, P(_p), P(C.c_size_t), P(C.c_size_t)]
+    if hasattr(L, "hs_flush_ordinals"):  # (A/B runs may load libraries built before round 6)
+        L.hs_flush_ordinals.argtypes = [_p, _p]
     L.hs_set_pose_log.argtypes = [_p, _p, _i, _i]
     L.hs_set_pose_log_slots.argtypes = [_p, _p, _p, _i, _i]
     L.hs_run_ranges_device.argtypes = [_p, _i, _p, _i, C.c_size_t, _p]

@@ -209,6 +209,17 @@ class HectorFleet:
             r["upd"] = u.reshape(sy, sx)
         return r
 
+    def flush_ordinals(self, hip_stream: int = 0):
+        """hs_flush_ordinals: every stream's 16-bit update ordinals into the int32 updateIndex plane now (zero-copy
+        readers of hs_get_device_buffers; replayed graph captures of *_device calls, at least every 32000 steps)."""
+        check(self.L.hs_flush_ordinals(self.h, C.c_void_p(hip_stream or None)), "hs_flush_ordinals")
+
+    def device_cells(self):
+        """(device pointer, bytes, stream_words) of the tiled cell storage (hs_get_device_buffers)."""
+        p, nb, sw = C.c_void_p(), C.c_size_t(), C.c_size_t()
+        check(self.L.hs_get_device_buffers(self.h, C.byref(p), C.byref(nb), C.byref(sw)), "hs_get_device_buffers")
+        return p.value, nb.value, sw.value
+
     def set_map(self, stream: int, level: int, logodds, upd):
         l = np.ascontiguousarray(logodds, np.float32)
         u = np.ascontiguousarray(upd, np.int32)

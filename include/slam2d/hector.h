@@ -39,6 +39,7 @@ extern "C" {
 #define HS_EHIP (-2)
 #define HS_ENOMEM (-3)
 #define HS_ENODEV (-4)
+#define HS_ESTATE (-5) /* the device state cannot be decoded as asked (hs_get_map after an ordinal overflow) */
 
 #define HS_MAX_LEVELS 8
 
@@ -178,11 +179,19 @@ int hs_get_diag_stamps(hs_ctx *ctx, int64_t out[8], int reset);
 /* Device cell storage (for zero-copy consumers): per stream `stream_words` 4-byte words; each level
  * is a grid of 64 x 32-cell tiles, each tile 20 KB = 2048 log-odds floats, then 2048 uint16 update
  * ordinals h, then 2048 int32 updateIndex values; inside a tile's plane the cells are stored in 4 x 4-cell
- * blocks, the blocks row-major (element of cell (lx, ly) = ((ly/4)*16 + lx/4)*16 + (ly%4)*4 + lx%4).  A cell's
- * updateIndex is 3*(E + (h-1)/2) + 1 + (h-1)%2 when h != 0 (E: the stream's ordinal epoch, advanced by the
- * library's periodic ordinal sweep), else the int32 plane's value; hs_get_map decodes it (DESIGN.md "Data
- * layout"). */
+ * blocks, the blocks row-major (element of cell (lx, ly) = ((ly/4)*16 + lx/4)*16 + (ly%4)*4 + lx%4).  The
+ * log-odds plane is always current.  A cell's updateIndex is 3*(E + (h-1)/2) + 1 + (h-1)%2 when h != 0, else
+ * the int32 plane's value; E (the stream's ordinal epoch) is internal, so a zero-copy reader of updateIndex
+ * first calls hs_flush_ordinals, after which every h is 0 and the int32 plane alone holds every cell's
+ * updateIndex.  hs_get_map decodes it without a flush (DESIGN.md "Data layout"). */
 int hs_get_device_buffers(hs_ctx *ctx, void **cells, size_t *cells_bytes, size_t *stream_words);
+/* Move every stream's 16-bit update ordinals into the int32 updateIndex plane now (the sweep the library runs by
+ * itself at least every 32000 steps; on hip_stream, NULL = the context's stream, ordered after the context's
+ * previous device work).  The library counts steps on the host to schedule its sweep: a caller that captures
+ * *_device calls into a HIP graph and replays it bypasses that count, and must call hs_flush_ordinals at least
+ * every 32000 replayed steps.  Past that bound a stream's ordinals no longer fit 16 bits: the device flags the
+ * stream, and hs_get_map returns HS_ESTATE for its updateIndex (never a wrapped value) until hs_reset. */
+int hs_flush_ordinals(hs_ctx *ctx, void *hip_stream);
 /* Optional device pose log: every step appends the scan-match pose (float3) of streams [0, streams)
  * at row = steps since hs_reset, i.e. d_buf[(row*streams + s)*3]; rows >= capacity are dropped.
  * d_buf NULL disables.  The caller owns d_buf (device memory of >= capacity*streams*3 floats). */

@@ -371,6 +371,157 @@ def test_reset(gpu, scans):
     _same_levels(fleet, ora, 2, "after reset")
 
 
+@pytest.mark.parametrize("sweep", ["1", "2", "3"])
+def test_reset_mid_run_with_sweeps(gpu, scans, monkeypatch, sweep):
+    """hs_reset between ordinal sweeps: the reset keeps the stream's update index and ordinal epoch
+    (GridMapBase::reset clears cells only) while the fill zeroes the hot ordinals and the cold plane, so the
+    updates after it must decode to the reference's updateIndex whatever the sweep phase -- every cell of both
+    levels bit-exact before and after the reset, with a sweep every 1, 2 or 3 steps."""
+    monkeypatch.setenv("SLAM2D_ORD_SWEEP", sweep)
+    fleet = HectorFleet(1, 0.05, 512, (0.5, 0.5), 2, max_points=1081)
+    ora = O.HectorOracle(0.05, 512, (0.5, 0.5), 2, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(-1.0, -1.0)
+    for k in range(4):
+        pts = scans.points[1, k, : scans.counts[1, k]]
+        fleet.update(0, pts)
+        ora.process(pts)
+    _same_levels(fleet, ora, 2, "before reset")
+    fleet.reset()
+    ora.reset()
+    for k in range(4, 9):
+        pts = scans.points[1, k, : scans.counts[1, k]]
+        gp, _, _ = fleet.update(0, pts)
+        op, _, _ = ora.process(pts)
+        np.testing.assert_array_equal(_bits(gp), _bits(op), err_msg=f"scan {k} after reset")
+    _same_levels(fleet, ora, 2, "after reset")
+
+
+def _dev_bytes(ptr, nbytes):
+    """nbytes of device memory at ptr, copied to the host with hipMemcpy (after a device synchronisation)."""
+    import ctypes
+
+    import torch
+
+    torch.cuda.synchronize()
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+    except OSError:
+        hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+    out = np.empty(nbytes, np.uint8)
+    rc = hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes), 2)
+    assert rc == 0, rc
+    return out
+
+
+def test_flush_ordinals_zero_copy(gpu, scans):
+    """hs_flush_ordinals: after it every 16-bit ordinal of the device cell storage is 0 and the int32
+    plane alone holds each cell's updateIndex, so a zero-copy reader of hs_get_device_buffers decodes without the
+    internal epoch: level 0 read raw from the device equals hs_get_map (log-odds and updateIndex); further updates
+    after the flush stay bit-exact vs the oracle."""
+    fleet = HectorFleet(1, 0.05, 512, (0.5, 0.5), 2, max_points=1081)
+    ora = O.HectorOracle(0.05, 512, (0.5, 0.5), 2, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(-1.0, -1.0)
+    for k in range(6):
+        pts = scans.points[2, k, : scans.counts[2, k]]
+        fleet.update(0, pts)
+        ora.process(pts)
+    want = fleet.get_map(0, 0)
+    fleet.flush_ordinals()
+    ptr, _, _ = fleet.device_cells()
+    sx, sy, _, _ = fleet.map_info(0)
+    tx, ty = (sx + 63) // 64, (sy + 31) // 32
+    raw = _dev_bytes(ptr, tx * ty * 20480).view(np.int32).reshape(ty, tx, 5120)  # level 0 is first in the stream
+    y, x = np.mgrid[0:sy, 0:sx]
+    e = ((y % 32) // 4 * 16 + (x % 64) // 4) * 16 + (y % 4) * 4 + x % 4  # element of the cell in its tile's planes
+    tile = raw[y // 32, x // 64]
+    logodds = np.take_along_axis(tile[..., :2048], e[..., None], -1)[..., 0]
+    ords = tile[..., 2048:3072].copy().view(np.uint16)
+    cold = np.take_along_axis(tile[..., 3072:], e[..., None], -1)[..., 0]
+    assert not ords.any(), "hot ordinals left after hs_flush_ordinals"
+    np.testing.assert_array_equal(cold, want["upd"])
+    np.testing.assert_array_equal(logodds, _bits(want["logodds"]))
+    for k in range(6, 9):
+        pts = scans.points[2, k, : scans.counts[2, k]]
+        gp, _, _ = fleet.update(0, pts)
+        op, _, _ = ora.process(pts)
+        np.testing.assert_array_equal(_bits(gp), _bits(op), err_msg=f"scan {k} after flush")
+    _same_levels(fleet, ora, 2, "after flush")
+
+
+def test_ordinal_overflow_is_refused(gpu, monkeypatch):
+    """A caller that never lets the library sweep (SLAM2D_ORD_SWEEP=0: the test knob standing for replayed graph
+    captures of *_device calls) drives a stream past 32767 map updates in one ordinal epoch: the device flags the
+    stream and hs_get_map refuses its updateIndex (HS_ESTATE) instead of decoding wrapped 16-bit ordinals; hs_reset
+    starts a fresh epoch, after which updates decode bit-exact vs the oracle again."""
+    import torch
+
+    monkeypatch.setenv("SLAM2D_ORD_SWEEP", "0")
+    size, n = 64, 16
+    a = np.linspace(0.0, 2 * np.pi, n, endpoint=False)
+    pts = (np.stack([np.cos(a), np.sin(a)], 1) * 20.0).astype(np.float32)  # map scale: 1 m rays on a 3.2 m map
+    fleet = HectorFleet(1, 0.05, size, (0.5, 0.5), 1, max_points=n)
+    ora = O.HectorOracle(0.05, size, (0.5, 0.5), 1, reduce_threads=T_RED)
+    for f in (fleet, ora):
+        f.set_update_factors(0.4, 0.9)
+        f.set_thresholds(-1.0, -1.0)
+    d_xy = torch.from_numpy(pts[None]).cuda()
+    d_n = torch.tensor([n], dtype=torch.int32).cuda()
+    steps = 32768  # the update k = 32767 needs ordinal 2 k + 2 = 65536
+    for _ in range(steps):
+        fleet.step_device(d_xy.data_ptr(), n, d_n.data_ptr())
+        ora.process(pts)
+    torch.cuda.synchronize()
+    with pytest.raises(Exception, match="code -5"):
+        fleet.get_map(0, 0)
+    fleet.reset()
+    ora.reset()
+    for _ in range(3):
+        fleet.update(0, pts)
+        ora.process(pts)
+    _same_levels(fleet, ora, 1, "after overflow + reset")
+
+
+@pytest.mark.parametrize("parts", ["1", "2"])
+def test_ordinal_sweep_part_streams(gpu, monkeypatch, parts):
+    """The ordinal sweep on the batched issue path with the fleet split over part streams (SLAM2D_PARTS=2: the
+    sweep runs on the context's stream before ev_start fans the step out to the part streams), a sweep
+    every 2 steps, 128 streams x 5 steps at 512^2 x 2 levels: poses of every step and every cell of sampled streams
+    bit-exact vs the oracle."""
+    import torch
+
+    monkeypatch.setenv("SLAM2D_ORD_SWEEP", "2")
+    monkeypatch.setenv("SLAM2D_PARTS", parts)
+    B, T = 128, 5
+    S = synth.make_streams(B, T, seed=71)
+    fleet = HectorFleet(B, 0.05, 512, (0.5, 0.5), 2, max_points=1081)
+    fleet.set_update_factors(0.4, 0.9)
+    fleet.set_thresholds(-1.0, -1.0)
+    check = [0, 63, 64, B - 1]  # both halves of a two-part split
+    oras = {s: O.HectorOracle(0.05, 512, (0.5, 0.5), 2, reduce_threads=T_RED) for s in check}
+    for o in oras.values():
+        o.set_update_factors(0.4, 0.9)
+        o.set_thresholds(-1.0, -1.0)
+    for t in range(T):
+        d_xy = _torch_dev(S.points[:, t])
+        d_n = _torch_dev(S.counts[:, t].astype(np.int32))
+        fleet.step_device(d_xy.data_ptr(), 1081, d_n.data_ptr())
+        torch.cuda.synchronize()
+        gp = fleet.poses()[0]
+        for s in check:
+            op, _, _ = oras[s].process(S.points[s, t, : S.counts[s, t]])
+            np.testing.assert_array_equal(_bits(gp[s]), _bits(op), err_msg=f"t={t} s={s}")
+    for s in check:
+        for lvl in range(2):
+            m = fleet.get_map(s, lvl)
+            ol, ou = oras[s].level(lvl)
+            np.testing.assert_array_equal(m["upd"], ou, err_msg=f"s={s} level {lvl} updateIndex")
+            np.testing.assert_array_equal(_bits(m["logodds"]), _bits(ol), err_msg=f"s={s} level {lvl} log-odds")
+
+
 def test_processor_mirror(gpu, scans):
     """HectorSlamProcessor mirror (reference API names) over DataContainer."""
     proc = HectorSlamProcessor(0.05, 1024, 1024, (0.5, 0.5), 2, max_points=1081)

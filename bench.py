@@ -750,12 +750,16 @@ def run_karto(args, world, rank, dev):
             # rate of the cache level that holds them (MI355X_MICROARCH.md, 'Indexed rows: gather into LDS':
             # rows shared by every workgroup from the XCD's L2 16.8-18.8 TB/s, a 38 MB table from the Infinity
             # Cache 8.6 TB/s), not against the HBM peak; the lower bound of the range is the peak used
+            # the level: every grid of the launch in one XCD's L2 (4 MiB); else each match's grid (read by that match's
+            # angle x tile workgroups, which run together) inside the 256 MiB Infinity Cache; else HBM
             grid_bytes = float(M) * float(info["grid_size"]) ** 2
-            level = "l2" if grid_bytes <= 4.0 * 2 ** 20 else ("infinity_cache" if grid_bytes <= 256.0 * 2 ** 20 else "hbm")
+            match_grid = float(info["grid_size"]) ** 2
+            level = "l2" if grid_bytes <= 4.0 * 2 ** 20 else ("infinity_cache" if match_grid <= 256.0 * 2 ** 20 else "hbm")
             peak = {"l2": 16800.0, "infinity_cache": 8600.0, "hbm": HBM_PEAK_GBS}[level]
             roof = {"bound": level, "kernel": "kt_coarse_kernel", "achieved": round(ach, 1),
                     "peak": peak, "unit": "GB/s", "frac": round(ach / peak, 4), "traffic": None,
                     "avg_launch_ms": round(coarse_ms / coarse_n, 5), "grid_bytes_per_launch": int(grid_bytes),
+                    "grid_bytes_per_match": int(match_grid),
                     "frac_of_hbm_peak": round(ach / HBM_PEAK_GBS, 4),
                     "note": "achieved = lookup bytes (1 B per pose x point) / launch time: a cache gather rate, not "
                             "DRAM traffic; peak = the guide's measured gather rate of the level holding the grids"}

@@ -4,8 +4,9 @@
 //
 // Data layout in HBM (per context):
 //   cells  : LogOddsCell {float l; int upd} (H/map/GridMapLogOdds.h:37-87) stored tiled: per stream,
-//            per level, 64 x 32-cell tiles of 16 KB each = [2048 log-odds floats][2048 updateIndex
-//            ints] (see hector_internal.h cell_word); the tile is the grid update's unit of work.
+//            per level, 64 x 32-cell tiles of 20 KB each = [2048 log-odds floats][2048 16-bit update
+//            ordinals][2048 updateIndex ints] (hector_internal.h cell_word, ORD_OFF, COLD_OFF: the grid update
+//            writes the ordinals, a periodic sweep the ints); the tile is the grid update's unit of work.
 //   state  : StreamState per stream (pose, last map-update pose, covariance, update indices).
 //   points : float2 per beam in level-0 map scale, padded to xy_stride per stream.
 //
@@ -18,8 +19,9 @@
 //                           each ray's cells inside a tile come from the closed-form Bresenham step
 //                           range, the once-per-scan semantics of bresenhamCellFree/Occ
 //                           (H/map/OccGridMapBase.h:302-330) are resolved in LDS event words, then
-//                           every marked cell's log-odds is read once and both planes written once
-//                           (the updateIndex plane is never read).  No global atomics; see DESIGN.md.
+//                           every marked cell's log-odds is read once and written once with its
+//                           16-bit update ordinal (neither index plane is read).  No global atomics;
+//                           see DESIGN.md.
 // Wrong-result pricing builds (no atomics, no walk, no apply, hardware exp) are not in this file:
 // tools/build_diag.py derives them from a copy of the sources.
 #include <hip/hip_runtime.h>

@@ -34,11 +34,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 
 CONFIGS = {
     # hector_slam.launch defaults (hector_slam.cc:138-142): 2048^2, 3 levels -- the north-star grid.
-    # 3840 streams x 52.5 MB pyramids (20-KB three-plane tiles) = 202 GB of HBM: three whole rounds of
-    # the match at 5 workgroups per CU
+    # 4608 streams x 52.5 MB pyramids (20-KB three-plane tiles) = 242 GB of HBM: three whole rounds of
+    # the match at 6 workgroups per CU (round 6; 3840 = three rounds at 5 per CU before).  One lease
+    # (profiles/r06/ab_r06k_match6_vs_prev.md): 1.958 M scans/s at 4608 vs 1.918 M at 3840 with the round-6 match;
+    # the round-5 match (5 per CU) read 1.892 M at 4608 and 1.906 M at 3840
     # (round 4, same lease: 1.58 M scans/s at 2560 streams, 1.64 M at 3840 -- the update's tail is a smaller
     # share of a longer launch; 1.48 M at 2048: profiles/r04/ab_r04d*.md, ab_r04h_3840.md, r04h_summary.md)
-    "northstar": dict(map_size=2048, levels=3, streams=3840),
+    "northstar": dict(map_size=2048, levels=3, streams=4608),
     # BASELINE configs[1]: single-res 1024^2.  3840 streams (10.5 MB each) = three whole rounds of the match at 5
     # workgroups per CU, like the north star; round 5, one lease: 1024 / 2560 / 3840 / 5120 streams -> 2.17 / 2.47 /
     # 2.53 / 2.49 M scans/s (profiles/r05/paths_r05m/)

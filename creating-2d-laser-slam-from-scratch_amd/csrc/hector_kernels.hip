@@ -830,8 +830,8 @@ __device__ __forceinline__ unsigned cell_off(const LevelGeom &g, unsigned x, uns
 
 template <int NP, bool BIG>
 __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
-                                           int n, float f, float *est, float &cs, float &sn, float *H, int parity,
-                                           unsigned *nb_key, float4 *nb_val, float (*s_pose)[POSE_WORDS], float *seqT,
+                                           int n, float f, float *est, float &cs, float &sn, int parity,
+                                           unsigned (&kreg)[NP], float4 *nb_val, float (*s_pose)[POSE_WORDS], float *seqT,
                                            int cw, int pt)
 {
     const int tid = threadIdx.x, lane = tid & 63;
@@ -842,17 +842,13 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
     unsigned short *wl0 = reinterpret_cast<unsigned short *>(seqT + (CW_BUFS - 1) * CW_BUF);  // the miss lists
     if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);
     if (wave != cw) {
-        // the gathered log-odds of the moved points (the transform is recomputed for the terms below: keeping
-        // px, py, fx, fy of every slot across the chunk loop cost more registers than 4 VALU per point)
-        float lg[NP][4];
+        // the moved points' neighbourhoods go straight from HBM into the cache planes by LDS-DMA (no VGPRs hold
+        // them; the transform is recomputed for the terms below)
         unsigned key[NP];
         bool miss[NP];
-        // every slot's key and its cached key first (the LDS reads in flight together), then the gathers of the
-        // moved points: one LDS latency before the first gather instead of one per slot
-        // (branch-free: a divergent branch here made the compiler wait for each LDS read before the next slot)
-        unsigned kv[NP];
-#pragma unroll
-        for (int j = 0; j < NP; ++j) kv[j] = nb_key[pt + j * CW_PTS];  // (every slot < CW_MAXN has a word)
+        // every slot's key first, then the gathers of the moved points (the cached keys are registers: a slot
+        // is only ever looked up by the thread that owns it)
+        const unsigned (&kv)[NP] = kreg;
         const float lim0 = g.lim[0], lim1 = g.lim[1];
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
@@ -864,41 +860,39 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
             const bool in = (slot < n) & (x >= 0.0f) & (x <= lim0) & (y >= 0.0f) & (y <= lim1);  // NaN -> out of map
             key[j] = in ? ((unsigned)(int)y << 16) | (unsigned)(int)x : NB_NONE;  // a slot >= n: no miss
         }
+        const int pw = pt >> 6;
+        float *nbf = reinterpret_cast<float *>(nb_val);  // four planes of CW_MAXN floats (cell 00, 10, 01, 11)
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
             miss[j] = key[j] != NB_NONE && kv[j] != key[j];
-            if (BIG && miss[j]) {
-                // (a level of 2^30 words or more -- maps above ~20000^2 cells, hs_match_kernel<.., .., true>:
-                // 64-bit addresses)
-                const int ux = (int)(key[j] & 0xFFFFu), uy = (int)(key[j] >> 16);
-                lg[j][0] = cells[cell_word(g, ux, uy)];
-                lg[j][1] = cells[cell_word(g, ux + 1, uy)];
-                lg[j][2] = cells[cell_word(g, ux, uy + 1)];
-                lg[j][3] = cells[cell_word(g, ux + 1, uy + 1)];
-            } else if (miss[j]) {
-                // 32-bit byte offsets from the level's (uniform) base: the gathers take the scalar-base +
-                // VGPR-offset form (cell_off)
+            if (miss[j]) {
+                // LDS-DMA: lane l of this wave lands at plane + (pw * 64 + j * CW_PTS) + l = its slot
+                const int sb = pw * 64 + j * CW_PTS;
                 const unsigned ux = key[j] & 0xFFFFu, uy = key[j] >> 16;
-                const char *cb = reinterpret_cast<const char *>(cells);
-                const float *r0 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy));
-                const float *r1 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy + 1u));
-                if ((ux & (CELL_BLK - 1)) != CELL_BLK - 1) {  // (ix, ix + 1) adjacent in a block row
-                    float2 a, b;
-                    __builtin_memcpy(&a, r0, 8);
-                    __builtin_memcpy(&b, r1, 8);
-                    lg[j][0] = a.x; lg[j][1] = a.y; lg[j][2] = b.x; lg[j][3] = b.y;
+                const float *a0, *a1, *a2, *a3;
+                if (BIG) {  // (levels of 2^30 words or more: 64-bit addresses)
+                    a0 = cells + cell_word(g, (int)ux, (int)uy);
+                    a1 = cells + cell_word(g, (int)ux + 1, (int)uy);
+                    a2 = cells + cell_word(g, (int)ux, (int)uy + 1);
+                    a3 = cells + cell_word(g, (int)ux + 1, (int)uy + 1);
                 } else {
-                    lg[j][0] = r0[0];
-                    lg[j][1] = *reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy));
-                    lg[j][2] = r1[0];
-                    lg[j][3] = *reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy + 1u));
+                    const char *cb = reinterpret_cast<const char *>(cells);
+                    a0 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy));
+                    a1 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy));
+                    a2 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux, uy + 1u));
+                    a3 = reinterpret_cast<const float *>(cb + 4u * cell_off(g, ux + 1u, uy + 1u));
                 }
+                typedef __attribute__((address_space(1))) void gv;
+                typedef __attribute__((address_space(3))) void lv;
+                __builtin_amdgcn_global_load_lds((gv *)a0, (lv *)(nbf + 0 * CW_MAXN + sb), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((gv *)a1, (lv *)(nbf + 1 * CW_MAXN + sb), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((gv *)a2, (lv *)(nbf + 2 * CW_MAXN + sb), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((gv *)a3, (lv *)(nbf + 3 * CW_MAXN + sb), 4, 0, 0);
             }
         }
         // park the gathered log-odds of every miss in its slot and list the slot for this wave (the list lives
         // in the last term buffer: with two, first written after chunk 0's barrier; with one, chunk 0 is stored
         // after a barrier that follows every wave's conversions), then convert 64 at a time
-        const int pw = pt >> 6;
         unsigned short *wl = reinterpret_cast<unsigned short *>(seqT + (CW_BUFS - 1) * CW_BUF) + pw * (NP * 64);
         int nmiss = 0;
 #pragma unroll
@@ -906,21 +900,22 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
             const int slot = pt + j * CW_PTS;
             const unsigned long long bm = __ballot(miss[j]);
             if (miss[j]) {
-                nb_val[slot] = make_float4(lg[j][0], lg[j][1], lg[j][2], lg[j][3]);
-                nb_key[slot] = key[j];
+                kreg[j] = key[j];
                 wl[nmiss + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] =
                     (unsigned short)slot;
             }
             nmiss += __popcll(bm);
         }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA landed (the barrier below publishes it)
         if constexpr (CW_SHARE) {
             if (lane == 0) s_mcnt[pw] = nmiss;
         } else {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            float *nbf = reinterpret_cast<float *>(nb_val);
             for (int e = lane; e < nmiss; e += 64) {
                 const int slot = wl[e];
-                const float4 v = nb_val[slot];
-                nb_val[slot] = make_float4(cell_prob(v.x), cell_prob(v.y), cell_prob(v.z), cell_prob(v.w));
+#pragma unroll
+                for (int c = 0; c < 4; ++c) nbf[c * CW_MAXN + slot] = cell_prob(nbf[c * CW_MAXN + slot]);
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
@@ -933,8 +928,9 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
         for (int e = tid; e < tot; e += MATCH_THREADS) {
             const int l = e < c0 ? 0 : (e < c0 + c1 ? 1 : 2);
             const int slot = wl0[l * (NP * 64) + e - (l == 0 ? 0 : (l == 1 ? c0 : c0 + c1))];
-            const float4 v = nb_val[slot];
-            nb_val[slot] = make_float4(cell_prob(v.x), cell_prob(v.y), cell_prob(v.z), cell_prob(v.w));
+            float *nbf = reinterpret_cast<float *>(nb_val);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) nbf[c * CW_MAXN + slot] = cell_prob(nbf[c * CW_MAXN + slot]);
         }
         lds_barrier();
     }
@@ -956,8 +952,9 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
                 if (pf.in) {
                     pf.fx = x - (float)(int)x;
                     pf.fy = y - (float)(int)y;
-                    const float4 v = nb_val[slot];
-                    pf.l[0] = v.x; pf.l[1] = v.y; pf.l[2] = v.z; pf.l[3] = v.w;
+                    const float *nbf = reinterpret_cast<const float *>(nb_val);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) pf.l[c] = nbf[c * CW_MAXN + slot];
                 }
                 point_terms<true>(pf, cs, sn, t);
             }
@@ -986,7 +983,7 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
     }
     float *sp = s_pose[parity];
     if (wave == cw) {
-        float s[9];
+        float s[9], H[9];
         seq_gather(run, s);
         float b[3] = {s[0], s[1], s[2]};
         H[0] = s[3]; H[4] = s[4]; H[8] = s[5];
@@ -1020,20 +1017,23 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
         __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
+    // (H stays in s_pose, read once at the level's end)
     est[0] = sp[0];
     est[1] = sp[1];
     est[2] = sp[2];
     cs = sp[3];
     sn = sp[4];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];
 }
 
 constexpr int MATCH_REG_PTS = 5;  // points per thread kept in registers: scans of up to 1280 points
 
-// register budget knob: waves per SIMD the compiler must fit the match kernel into (1 = unconstrained)
+// register budget of the reference-order register instances (gn_step_cw): waves per SIMD the compiler must fit
+// them into.  6 (default, round 6): 80 VGPRs; with the cache keys in registers and the gathers by LDS-DMA the
+// instance needs 26.1 KB of LDS, so six workgroups share a CU (5 before: 31.3 KB, 89 VGPRs).  Measured
+// (profiles/r06/ab_r06h*, ab_r06i*): match -1.9 % at the north star, -2.9 % under the node's gate; the
+// other instances (tree order, HBM path) stay unconstrained (1)
 #ifndef S2D_MATCH_WAVES
-#define S2D_MATCH_WAVES 1
+#define S2D_MATCH_WAVES 6
 #endif
 // SEQ (default): H / b summed in the reference's sequential point order; else the tree order
 // (SLAM2D_MATCH_ORDER=tree / hs_set_reduction_order: faster, poses within float reassociation of the
@@ -1044,7 +1044,7 @@ constexpr int MATCH_REG_PTS = 5;  // points per thread kept in registers: scans 
 // BIG: some level holds 2^30 words or more (maps above ~20000^2 cells): the reference-order gathers use 64-bit
 // addresses (cell_word) instead of 32-bit byte offsets from the level base (cell_off)
 template <bool SEQ, bool REGS, bool BIG>
-__global__ void __launch_bounds__(MATCH_THREADS) __attribute__((amdgpu_waves_per_eu(S2D_MATCH_WAVES)))
+__global__ void __launch_bounds__(MATCH_THREADS) __attribute__((amdgpu_waves_per_eu((SEQ && REGS) ? S2D_MATCH_WAVES : 1)))
 hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__restrict__ state,
                 const float2 *__restrict__ xy, int xy_stride, const int *__restrict__ counts,
                 const float2 *__restrict__ origo, const float *__restrict__ hints, int stream_begin, int mode,
@@ -1060,7 +1060,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
     constexpr int NSLOT = CW ? CW_MAXN : MATCH_REG_PTS * MATCH_THREADS;
     constexpr int SEQ_LDS = !CW ? SEQ_WORDS : ((CW_BUFS * CW_BUF > SEQ_WORDS || REGS) ? CW_BUFS * CW_BUF : SEQ_WORDS);
     __shared__ __attribute__((aligned(16))) float seqT[SEQ ? SEQ_LDS : 4];
-    __shared__ unsigned nb_key[NSLOT];
+    __shared__ unsigned nb_key[CW ? 4 : NSLOT];  // (the chain-wave path keeps its cached keys in registers: kreg)
     __shared__ float4 nb_val[NSLOT];
     __shared__ unsigned short mlist[CW ? 4 : MATCH_REG_PTS * MATCH_THREADS];  // tree order: per wave, the slots whose cell moved
     __shared__ float s_pose[2][POSE_WORDS];                             // a step's result, by parity
@@ -1116,6 +1116,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
         const int pstride = CW ? CW_PTS : MATCH_THREADS;
         const bool in_regs = n <= pstride * NPR;
         float2 preg[NPR];
+        unsigned kreg[NPR];  // CW: each owned slot's neighbourhood-cache key (NB_NONE: nothing cached)
 #pragma unroll
         for (int j = 0; j < NPR; ++j) {
             const int i = pt + j * pstride;
@@ -1151,14 +1152,16 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
             float est[3], H[9];
             map_from_world(g, tmp, est);
 #pragma unroll
-            for (int j = 0; j < NPR; ++j)
-                if (owner) nb_key[pt + j * pstride] = NB_NONE;  // own slots
+            for (int j = 0; j < NPR; ++j) {
+                if constexpr (CW) kreg[j] = NB_NONE;
+                else if (owner) nb_key[pt + j * pstride] = NB_NONE;  // own slots
+            }
             float cs = sdm_cosf(est[2]), sn = sdm_sinf(est[2]);
             for (int it = 0; it <= iters; ++it) {
                 if (in_regs) {
                     if constexpr (CW)
-                        gn_step_cw<NPR, BIG>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, parity, nb_key, nb_val, s_pose, seqT,
-                                        cw, pt);
+                        gn_step_cw<NPR, BIG>(lc, g, preg, n, g.pts_scale, est, cs, sn, parity, kreg, nb_val, s_pose, seqT,
+                                             cw, pt);
                     else
                         gn_step_reg<NPR, SEQ>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, red, parity, nb_key,
                                               nb_val, mlist, s_pose, seqT);
@@ -1169,8 +1172,9 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
                 parity ^= 1;
             }
             est[2] = normalize_angle(est[2]);
+            // the last step's H: the chain-wave path left it in s_pose only (parity has moved past it)
 #pragma unroll
-            for (int k = 0; k < 9; ++k) cov[k] = H[k];
+            for (int k = 0; k < 9; ++k) cov[k] = (CW && in_regs) ? s_pose[parity ^ 1][5 + k] : H[k];
             cov_h = true;
             world_from_map(g, est, tmp);
         }

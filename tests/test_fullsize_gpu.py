@@ -1,7 +1,7 @@
 """GPU parity at the BASELINE.json configs' full sizes (c3 and GMapping at 1024 particles had
 no GPU test, the Karto loop window was tested below its benched size).
 
-  * north star -- the bench's fleet shape, 3840 streams x 2048^2 x 3 levels (202 GB), default issue path;
+  * north star -- the bench's fleet shape, 4608 streams x 2048^2 x 3 levels (242 GB), default issue path;
   * c3  -- lesson4 hector_slam 3-level 4096 x 4096 grid, a fleet of 1024 streams (225 GB of maps, so
            the last stream's cells sit above 2^32 words): streams 0, 511, 512 (the second fleet half of
            hs_run_ranges_device) and 1023 replayed on the oracle, poses every step and every cell of all
@@ -97,19 +97,19 @@ def test_c3_4096x3_fleet_last_stream_bitexact(gpu, monkeypatch, request, pipelin
 
 
 def test_north_star_fleet_shape_bitexact(gpu, request):
-    """The bench's own north-star shape (bench.py CONFIGS["northstar"]): 3840 streams x 2048^2 x 3 levels (202 GB
-    of pyramids, three whole rounds of the match at 5 workgroups per CU), raw ranges through
+    """The bench's own north-star shape (bench.py CONFIGS["northstar"]): 4608 streams x 2048^2 x 3 levels (242 GB
+    of pyramids, three whole rounds of the match at 6 workgroups per CU), raw ranges through
     hs_run_ranges_device with the default issue path, stream pad and update split, forced map update -- 4 steps.
     Poses of every 64th stream and the last (the bench's pose log) equal the oracle in the reference order bit for
     bit at every step, and every cell of all three levels of the first, middle and last streams."""
     import torch
 
-    B, LV, SIZE, T = 3840, 3, 2048, 4
+    B, LV, SIZE, T = 4608, 3, 2048, 4
     S = synth.make_streams(B, T, seed=5150)
     nb = S.ranges.shape[2]
     ang = synth.beam_angles(nb)
     fleet = HectorFleet(B, 0.05, SIZE, (0.5, 0.5), LV, max_points=1081)
-    request.addfinalizer(fleet.close)  # 202 GB: free it even when an assertion fails
+    request.addfinalizer(fleet.close)  # 242 GB: free it even when an assertion fails
     fleet.set_update_factors(0.4, 0.9)
     fleet.set_thresholds(-1.0, -1.0)
     fleet.set_laser(HsLaser.defaults(nb, float(ang[0]), float(ang[1] - ang[0])),

@@ -167,18 +167,18 @@ PATCHES = {
     "mclk": [(K, "template <int NP, bool BIG>\n__device__ __forceinline__ void gn_step_cw(",
               "extern __device__ unsigned long long g_stamps[8];\n__shared__ unsigned long long s_mk[8];\n"
               "template <int NP, bool BIG>\n__device__ __forceinline__ void gn_step_cw("),
-             (K, "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds",
+             (K, "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the moved points' neighbourhoods",
               "    unsigned long long mk_t0 = __builtin_amdgcn_s_memtime(), mk_t1 = 0, mk_t2 = 0, mk_pa = 0, mk_pb = 0, mk_pc = 0; bool mk_big = false;\n"
-              "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the gathered log-odds"),
+              "    if (S2D_PRECHAIN_PRIO) __builtin_amdgcn_s_setprio(S2D_PRECHAIN_PRIO);\n    if (wave != cw) {\n        // the moved points' neighbourhoods"),
              (K, "            lds_barrier();\n            if (lane < 9)\n                run = seq_chain_t<CW_STRIDE>(",
               "            lds_barrier();\n            if (j == 0) mk_t1 = __builtin_amdgcn_s_memtime();\n            if (lane < 9)\n                run = seq_chain_t<CW_STRIDE>("),
-             (K, "                                             run);\n        }\n    }\n    float *sp = s_pose[parity];\n    if (wave == cw) {\n        float s[9];",
-              "                                             run);\n        }\n        mk_t2 = __builtin_amdgcn_s_memtime();\n    }\n    float *sp = s_pose[parity];\n    if (wave == cw) {\n        float s[9];"),
-             (K, "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS",
+             (K, "                                             run);\n        }\n    }\n    float *sp = s_pose[parity];\n    if (wave == cw) {\n        float s[9], H[9];",
+              "                                             run);\n        }\n        mk_t2 = __builtin_amdgcn_s_memtime();\n    }\n    float *sp = s_pose[parity];\n    if (wave == cw) {\n        float s[9], H[9];"),
+             (K, "    __syncthreads();\n    // (H stays in s_pose, read once at the level's end)\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n}\n\nconstexpr int MATCH_REG_PTS",
               "    if (wave == cw && lane == 0) {\n        const unsigned long long mk_t3 = __builtin_amdgcn_s_memtime();\n"
               "        s_mk[0] += mk_t1 - mk_t0; s_mk[1] += mk_t2 - mk_t1; s_mk[2] += mk_t3 - mk_t2;\n    }\n"
               "    if (wave != cw && pt == 0) { s_mk[4] += mk_pa - mk_t0; s_mk[5] += mk_pb - mk_pa; s_mk[6] += mk_pc - mk_pb; if (mk_big) s_mk[7] += mk_pb - mk_pa; }\n"
-              "    __syncthreads();\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n#pragma unroll\n    for (int k = 0; k < 9; ++k) H[k] = sp[5 + k];\n}\n\nconstexpr int MATCH_REG_PTS"),
+              "    __syncthreads();\n    // (H stays in s_pose, read once at the level's end)\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n}\n\nconstexpr int MATCH_REG_PTS"),
              (K, "        if constexpr (CW_SHARE) {\n            if (lane == 0) s_mcnt[pw] = nmiss;",
               "        mk_pa = __builtin_amdgcn_s_memtime();\n        if constexpr (CW_SHARE) {\n            if (lane == 0) s_mcnt[pw] = nmiss;"),
              (K, "        lds_barrier();\n    }\n    if (wave != cw) {\n        // chunk j = slot j",

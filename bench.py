@@ -41,10 +41,10 @@ CONFIGS = {
     # (round 4, same lease: 1.58 M scans/s at 2560 streams, 1.64 M at 3840 -- the update's tail is a smaller
     # share of a longer launch; 1.48 M at 2048: profiles/r04/ab_r04d*.md, ab_r04h_3840.md, r04h_summary.md)
     "northstar": dict(map_size=2048, levels=3, streams=4608),
-    # BASELINE configs[1]: single-res 1024^2.  3840 streams (10.5 MB each) = three whole rounds of the match at 5
-    # workgroups per CU, like the north star; round 5, one lease: 1024 / 2560 / 3840 / 5120 streams -> 2.17 / 2.47 /
-    # 2.53 / 2.49 M scans/s (profiles/r05/paths_r05m/)
-    "c2": dict(map_size=1024, levels=1, streams=3840),
+    # BASELINE configs[1]: single-res 1024^2.  4608 streams (10.5 MB each) = three whole rounds of the match at 6
+    # workgroups per CU, like the north star (round 6, one lease: 3840 -> 2.459 M, 4608 -> 2.486 M scans/s,
+    # profiles/r06/ab_r06n_c2_fleet.md; round 5 at 5 per CU: 1024 / 2560 / 3840 / 5120 -> 2.17 / 2.47 / 2.53 / 2.49 M)
+    "c2": dict(map_size=1024, levels=1, streams=4608),
     # BASELINE configs[2]: 3-level 4096^2
     "c3": dict(map_size=4096, levels=3, streams=1024),  # 1024 x 220 MB pyramids = 225 GB of HBM
 }

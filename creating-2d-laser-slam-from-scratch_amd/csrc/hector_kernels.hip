@@ -832,7 +832,7 @@ template <int NP, bool BIG>
 __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, const LevelGeom &g, const float2 (&p)[NP],
                                            int n, float f, float *est, float &cs, float &sn, int parity,
                                            unsigned (&kreg)[NP], float4 *nb_val, float (*s_pose)[POSE_WORDS], float *seqT,
-                                           int cw, int pt)
+                                           int cw, int pt, bool first)
 {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = tid >> 6;
@@ -901,13 +901,19 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
             const unsigned long long bm = __ballot(miss[j]);
             if (miss[j]) {
                 kreg[j] = key[j];
-                wl[nmiss + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] =
-                    (unsigned short)slot;
+                // (a first step keeps no list: its terms may already fill the buffer the lists live in)
+                if (!first)
+                    wl[nmiss + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u))] =
+                        (unsigned short)slot;
             }
             nmiss += __popcll(bm);
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA landed (the barrier below publishes it)
-        if constexpr (CW_SHARE) {
+        if (first) {
+            // a level's first step: every in-map point missed (the keys were reset); each point thread converts its
+            // own slots chunk by chunk below, so chunk 0's terms -- and the chain -- start after one sixth of the
+            // conversions, and chunk j + 1's overlap the chain's chunk j
+        } else if constexpr (CW_SHARE) {
             if (lane == 0) s_mcnt[pw] = nmiss;
         } else {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -920,7 +926,7 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
     }
-    if constexpr (CW_SHARE) {
+    if (CW_SHARE && !first) {
         // every wave converts entries wave * 64 + lane + 256 k of the three lists laid end to end; the second
         // barrier also retires the lists before chunk 0's terms overwrite them
         lds_barrier();
@@ -952,9 +958,16 @@ __device__ __forceinline__ void gn_step_cw(const float *__restrict__ cells, cons
                 if (pf.in) {
                     pf.fx = x - (float)(int)x;
                     pf.fy = y - (float)(int)y;
-                    const float *nbf = reinterpret_cast<const float *>(nb_val);
+                    float *nbf = reinterpret_cast<float *>(nb_val);
 #pragma unroll
                     for (int c = 0; c < 4; ++c) pf.l[c] = nbf[c * CW_MAXN + slot];
+                    if (first) {  // this thread's own gathered log-odds (its LDS-DMA landed: vmcnt(0) above)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            pf.l[c] = cell_prob(pf.l[c]);
+                            nbf[c * CW_MAXN + slot] = pf.l[c];
+                        }
+                    }
                 }
                 point_terms<true>(pf, cs, sn, t);
             }
@@ -1161,7 +1174,7 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
                 if (in_regs) {
                     if constexpr (CW)
                         gn_step_cw<NPR, BIG>(lc, g, preg, n, g.pts_scale, est, cs, sn, parity, kreg, nb_val, s_pose, seqT,
-                                             cw, pt);
+                                             cw, pt, it == 0);
                     else
                         gn_step_reg<NPR, SEQ>(lc, g, preg, n, g.pts_scale, est, cs, sn, H, red, parity, nb_key,
                                               nb_val, mlist, s_pose, seqT);

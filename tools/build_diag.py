@@ -179,8 +179,8 @@ PATCHES = {
               "        s_mk[0] += mk_t1 - mk_t0; s_mk[1] += mk_t2 - mk_t1; s_mk[2] += mk_t3 - mk_t2;\n    }\n"
               "    if (wave != cw && pt == 0) { s_mk[4] += mk_pa - mk_t0; s_mk[5] += mk_pb - mk_pa; s_mk[6] += mk_pc - mk_pb; if (mk_big) s_mk[7] += mk_pb - mk_pa; }\n"
               "    __syncthreads();\n    // (H stays in s_pose, read once at the level's end)\n    est[0] = sp[0];\n    est[1] = sp[1];\n    est[2] = sp[2];\n    cs = sp[3];\n    sn = sp[4];\n}\n\nconstexpr int MATCH_REG_PTS"),
-             (K, "        if constexpr (CW_SHARE) {\n            if (lane == 0) s_mcnt[pw] = nmiss;",
-              "        mk_pa = __builtin_amdgcn_s_memtime();\n        if constexpr (CW_SHARE) {\n            if (lane == 0) s_mcnt[pw] = nmiss;"),
+             (K, "        if (first) {\n            // a level's first step",
+              "        mk_pa = __builtin_amdgcn_s_memtime();\n        if (first) {\n            // a level's first step"),
              (K, "        lds_barrier();\n    }\n    if (wave != cw) {\n        // chunk j = slot j",
               "        lds_barrier();\n    }\n    mk_pb = __builtin_amdgcn_s_memtime();\n    if (wave != cw) {\n        // chunk j = slot j"),
              (K, "            lds_barrier();  // chunk j stored (two buffers: and the chain wave is done with chunk j - 1)\n",

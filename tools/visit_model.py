@@ -47,6 +47,7 @@ def main():
     nscans = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     ss = synth.make_streams(nscans, 1, distinct_paths=nscans)
     tot = np.zeros((3, 7))
+    segs = np.zeros(3)
     bal = {(lvl, nw): np.zeros(4) for lvl in range(3) for nw in (4, 2)}
     for k in range(nscans):
         pts = ss.points[k, 0, :ss.counts[k, 0]]
@@ -61,7 +62,7 @@ def main():
             bx0, bx1 = min(x0, x1.min()) // TILE, max(x0, x1.max()) // TILE
             by0, by1 = min(y0, y1.min()) // TILE_H, max(y0, y1.max()) // TILE_H
             ntiles = (bx1 - bx0 + 1) * (by1 - by0 + 1)
-            ballot = setup = useful = cone_pass = cone_setup = 0
+            ballot = setup = useful = cone_pass = cone_setup = seg_setup = 0
             lanes_setup = lanes_useful = 0
             for g in range(0, n, 64):
                 idx = np.arange(g, min(g + 64, n))
@@ -78,6 +79,18 @@ def main():
                         own = [i for i in gv if max(x0, x1[i]) >= X0 and min(x0, x1[i]) < X0 + TILE and
                                max(y0, y1[i]) >= Y0 and min(y0, y1[i]) < Y0 + TILE_H]
                         use = [i for i in own if (tx, ty) in tiles_of[i]]
+                        # segment test (round 6): the lane's ray line against the tile's integer box; a Bresenham cell
+                        # lies within |cross| < (da + 1) / 2 of the line, so all four corners beyond +-da on one side
+                        # means no cell of the ray in the tile (conservative)
+                        seg = []
+                        for i in own:
+                            ddx, ddy = int(x1[i] - x0), int(y1[i] - y0)
+                            da_ = max(abs(ddx), abs(ddy))
+                            cr = [ddx * (cy - y0) - ddy * (cx - x0) for cx in (X0, X0 + TILE - 1) for cy in (Y0, Y0 + TILE_H - 1)]
+                            if not (min(cr) > da_ or max(cr) < -da_):
+                                seg.append(i)
+                        assert set(use) <= set(seg), "segment test rejected a ray with steps in the tile"
+                        seg_setup += bool(seg)
                         cm = bool(cone_meets(w, X0 - x0, X0 + TILE - 1 - x0, Y0 - y0, Y0 + TILE_H - 1 - y0))
                         cone_pass += cm
                         if own:
@@ -88,6 +101,7 @@ def main():
                         if use:
                             useful += 1
             tot[lvl] += [ntiles, ballot, setup, useful, cone_setup, lanes_setup, lanes_useful]
+            segs[lvl] += seg_setup
             # wave balance: per (tile, fan group) the clip setup and the longest walk of its lanes in the tile
             for th, nw in ((TILE_H, 4), (TILE_H // 2, 2)):
                 cost = {}  # tile -> per-wave cost
@@ -121,6 +135,8 @@ def main():
         t = tot[lvl] / nscans
         print(f"{lvl:5d} {t[0]:10.0f} {t[1]:13.0f} {t[2]:7.0f} {t[3]:14.0f} {t[4]:18.0f} {t[5] / max(t[2], 1):12.1f} "
               f"{t[6] / max(t[2], 1):19.1f}")
+    print("setups surviving the segment test (some lane's ray line meets the tile's box; round 6):",
+          ", ".join(f"level {lvl}: {segs[lvl] / nscans:.0f}" for lvl in range(3)))
     print(f"wave balance (model: {SETUP} per clip setup + {STEP} per walk step; busiest wave / mean wave, summed over tiles):")
     print("level  4 waves x 64x32: busiest/mean  tiles<=2 groups  raster per tile (busiest)  |  2 waves x 64x16: busiest/mean  "
           "raster per 64x32 area (busiest)")

@@ -50,6 +50,8 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
                             log of the ordinal plane, round-6 VERDICT item 1; the fold kernel is priced separately)
   ordbm2     WRONG RESULTS  ordbm without the header store and the any-mark test: every thread of a tile with marks stores
                             its 2-B bit word (the floor of a bitmap log's store cost in the update)
+  valu100    same results   hs_update_kernel issues 100 extra independent v_add_f32 per tile iteration per wave (prices the
+                            kernel's sensitivity to VALU issue: ~+40 % of its VALU instructions)
   ordfull    WRONG RESULTS  hs_update_kernel stores every marked quad's four ordinals in one 8-B store, unmarked cells
                             included (prices per-cell 2-B stores against one store per quad)
   uclk       same results   hs_update_kernel's waves sum s_memtime cycles per tile-loop phase (raster, load/store wait,
@@ -147,6 +149,9 @@ PATCHES = {
                 "                    const unsigned mk = ((u >> 7) & 1u) | ((u >> 14) & 2u) | ((u >> 21) & 4u) | (u >> 28);\n"
                 "                    bm |= (mk | (qb_hits(qb[j]) << 3)) << (8 * j);\n                }\n"
                 "                tu[qtid] = (unsigned short)(bm | (mark_free << 16));\n            }\n            pend_tl = nullptr;\n")],
+    "valu100": [(K, "        const int X0 = tx * TILE, Y0 = ty * UPD_TH;\n",
+                 "        const int X0 = tx * TILE, Y0 = ty * UPD_TH;\n"
+                 "        { float dmy_; asm volatile(\".rept 100\\n\\tv_add_f32 %0, %1, %2\\n\\t.endr\" : \"=v\"(dmy_) : \"v\"((float)X0), \"v\"((float)Y0)); }\n")],
     "ordfull": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n",
                  "                *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n")],
     "uclk": [(K, "    for (int ii = 0; ii <= my_tiles; ++ii) {\n        const int i = __builtin_amdgcn_readfirstlane(ii);  // uniform (the compiler had put it in a VGPR)\n        const int qtid = tid;",

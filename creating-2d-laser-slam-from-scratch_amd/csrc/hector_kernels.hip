@@ -1282,7 +1282,14 @@ hs_match_kernel(FleetGeom geom, const float *__restrict__ cells, StreamState *__
 // Every ray starts at the common begin cell; a ray is stored as its end cell (packed y<<16 | x) or
 // RAY_INVALID when updateByScan would skip it (begin == end :157, or begin/end outside :226-238).
 constexpr unsigned RAY_INVALID = 0xFFFFFFFFu;
-constexpr int UPD_THREADS = 256;
+// waves per hs_update_kernel workgroup: 4 (default: 256 threads, 64 x 32-cell LDS tiles, 8 workgroups per CU) or 8
+// (512 threads, 64 x 64-cell tiles, 4 per CU: the same 32 waves per CU, half the tile visits and clip setups)
+#ifndef S2D_UPD_WAVES
+#define S2D_UPD_WAVES 4
+#endif
+constexpr int UPD_WAVES = S2D_UPD_WAVES;
+static_assert(UPD_WAVES == 4 || UPD_WAVES == 8, "hs_update_kernel: 4 or 8 waves per workgroup");
+constexpr int UPD_THREADS = 64 * UPD_WAVES;
 // two LDS words per tile cell, both updated with blind atomicMin (no read-modify-write chain):
 //   first_hit[c]  = smallest beam whose end cell is c      (NONE if none)
 //   first_free[c] = smallest beam that frees c            (NONE if none)
@@ -1947,10 +1954,11 @@ constexpr int UPD_STRIDE = S2D_UPD_STRIDE;
 #define S2D_APPLY_FAST 1  // 0: every marked quad takes the full apply_cell sequence (A/B)
 #endif
 #ifndef S2D_UPD_TH
-#define S2D_UPD_TH 32
+#define S2D_UPD_TH (8 * S2D_UPD_WAVES)  // 32 rows with 4 waves, 64 with 8: every thread owns two quads of a tile
 #endif
 #ifndef S2D_UPD_MINB
-#define S2D_UPD_MINB 8  // __launch_bounds__ min workgroups per CU: 8 x 4 waves caps the VGPRs at 64 (full occupancy)
+#define S2D_UPD_MINB 8  // __launch_bounds__ minimum: 8 waves per SIMD, which caps the VGPRs at 64 (full occupancy; with 8-wave
+                        // workgroups the value 4 let the compiler settle for 7 waves per SIMD, i.e. 3 workgroups per CU)
 #endif
 constexpr int UPD_TH = S2D_UPD_TH;                    // LDS tile height (a multiple of the storage TILE_H)
 static_assert(UPD_TH % TILE_H == 0, "an LDS tile covers whole storage tiles");
@@ -2118,7 +2126,10 @@ __device__ __forceinline__ int fan_beam(int b0, int lane)  // b0 = 256 G + 64 w
     return b0 + 2 * (lane & 31) + (lane >> 5);
 #endif
 }
-__host__ __device__ constexpr int fan_groups(int max_points) { return ((max_points + 255) / 256) * 4; }
+__host__ __device__ constexpr int fan_groups(int max_points)
+{
+    return ((max_points + UPD_THREADS - 1) / UPD_THREADS) * UPD_WAVES;
+}
 constexpr int UPD_GROUP_WORDS = 4;  // LDS words per fan group: its bounding box
 
 // Grid: for level l, upd_parts[l] x count blocks (level-major, then part, then stream); part p of a
@@ -2128,7 +2139,8 @@ constexpr int UPD_GROUP_WORDS = 4;  // LDS words per fan group: its bounding box
 // at 1081 beams, 8 instead of 7 workgroups per CU (the kernel's VGPRs allow 8).  RREG = 0: rays in LDS.
 // The rays are five named registers picked by selects on the wave-uniform fan-group index (an array
 // or a struct indexed by it ends up in scratch).
-constexpr int UPD_RREG = 5;
+constexpr int UPD_RREG = (1280 + UPD_THREADS - 1) / UPD_THREADS;  // scans of <= 1280 (4 waves) / 1536 (8) points
+static_assert(UPD_RREG <= 5, "five ray registers at most");
 template <int RREG>
 __global__ void __launch_bounds__(UPD_THREADS, S2D_UPD_MINB)
 hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restrict__ state,
@@ -2194,7 +2206,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
     // the wave's first beam in a scalar register: the fan-group loops and the ray-register selects below
     // then compile to scalar control (tid & ~63 in a VGPR made them divergent loops with exec-mask code)
     const int wave_beam0 = __builtin_amdgcn_readfirstlane(tid & ~63);
-    for (int b0 = wave_beam0; (b0 & ~255) < n; b0 += UPD_THREADS) {   // wave-uniform trip count
+    for (int b0 = wave_beam0; (b0 & ~(UPD_THREADS - 1)) < n; b0 += UPD_THREADS) {   // wave-uniform trip count
         const int b = fan_beam(b0, lane);
         unsigned r = RAY_INVALID;
         if (b < n) {
@@ -2202,12 +2214,12 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             if constexpr (RREG == 0) rays[b] = r;
         }
         if constexpr (RREG > 0) {
-            const int k = b0 >> 8;
+            const int k = (int)((unsigned)b0 / UPD_THREADS);
             rr0 = k == 0 ? r : rr0;
             rr1 = k == 1 ? r : rr1;
             rr2 = k == 2 ? r : rr2;
-            rr3 = k == 3 ? r : rr3;
-            rr4 = k == 4 ? r : rr4;
+            rr3 = (RREG > 3 && k == 3) ? r : rr3;  // (8 waves: three registers)
+            rr4 = (RREG > 4 && k == 4) ? r : rr4;
         }
         int gx0 = x0, gy0 = y0, gx1 = x0, gy1 = y0;  // fan group box: origin + valid ends
         if (r != RAY_INVALID) {
@@ -2310,7 +2322,8 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
             {
                 // this wave's groups (fi = wave + 4 k) among the first 64 that meet the tile, one set bit each:
                 // the loop visits only those (scalar find-first-set), then the groups past 64 test their box
-                unsigned long long gm = fm & (0x1111111111111111ull << (wave_beam0 >> 6));
+                unsigned long long gm = fm & ((UPD_WAVES == 8 ? 0x0101010101010101ull : 0x1111111111111111ull)
+                                              << (wave_beam0 >> 6));
                 int b0x = wave_beam0 + 64 * 64;  // groups >= 64 (scans of > 4096 points)
                 if constexpr (S2D_UPD_PRIO) {
                     // the waves with more of this tile's groups issue first: the four meet at the tile's barrier,
@@ -2326,7 +2339,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                         b0 = __builtin_ctzll(gm) << 6;
                         gm &= gm - 1ull;
                     } else {
-                        if ((b0x & ~255) >= n) break;
+                        if ((b0x & ~(UPD_THREADS - 1)) >= n) break;
                         b0 = b0x;
                         b0x += UPD_THREADS;
                         const int4 gb = gbox[b0 >> 6];
@@ -2337,7 +2350,7 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                     const int b = fan_beam(b0, lane);
                     unsigned r;
                     if constexpr (RREG > 0) {
-                        const int k = b0 >> 8;
+                        const int k = (int)((unsigned)b0 / UPD_THREADS);
                         r = k == 0 ? rr0 : (k == 1 ? rr1 : (k == 2 ? rr2 : (k == 3 ? rr3 : rr4)));
                     }
                     else r = b < n ? rays[b] : RAY_INVALID;
@@ -2441,6 +2454,10 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 if (!qb_any(mb)) continue;
                 const int qi = qtid + j * UPD_THREADS;
                 const unsigned o = (unsigned)upd_off(qi >> 4, (qi & 15) << 2, g.tiles_x);
+                // the quad's ordinals, in 16-bit units from this tile block's plane: an LDS tile taller than a storage
+                // tile continues in the block below, whose plane is one block (2 x TILE_BLOCK_WORDS halves) further
+                const unsigned ou = UPD_TH == TILE_H ? o
+                                                     : o + (unsigned)((qi >> 4) / TILE_H * g.tiles_x * TILE_BLOCK_WORDS);
                 float4 v = ql[j];
                 const float lv[4] = {v.x, v.y, v.z, v.w};
                 float nv[4];
@@ -2473,11 +2490,11 @@ hs_update_kernel(FleetGeom geom, float *__restrict__ cells, StreamState *__restr
                 // per marked cell (its unmarked cells were never read)
                 upd_store(reinterpret_cast<float4 *>(&pend_tl[o]), make_float4(nv[0], nv[1], nv[2], nv[3]));
                 if (qb_all(mb)) {
-                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));
+                    *reinterpret_cast<uint2 *>(&tu[ou]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));
                 } else {
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];
+                        if (qb_cell(mb, c)) tu[ou + (unsigned)c] = (unsigned short)uv[c];
                 }
                 touched += qb_count(mb);
             }

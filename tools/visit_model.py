@@ -13,7 +13,11 @@ SETUP instructions per (tile, group) clip setup plus STEP per step of the longes
 in that tile.  The barrier after the raster makes the busiest wave the tile's path, so the model prints, per
 level, sum over tiles of the busiest wave's cost / sum of the mean wave's cost, the share of tiles (with steps)
 crossed by <= 2 fan groups, and the same ratio for two alternatives: two-wave workgroups on 64 x 16 tiles
-(groups fi = w, w + 2, ...), whose busiest wave summed over a 64 x 32 area is the last column.
+(groups fi = w, w + 2, ...), whose busiest wave summed over a 64 x 32 area is the last column; eight-wave
+workgroups on 64 x 64 tiles; and the wave-slot time (waves x busiest wave) of those and of four waves sharing a
+tile crossed by one or two groups (each group's walks split over 4 / G waves).  Both of the latter were built and
+measured slower (profiles/r06/ab_r06y_update_8waves.md: +26 %, ab_r06z_update_split.md: +16.5 %), so neither the
+busiest-wave nor the slot-time reading of this model predicts the kernel.
 """
 import os
 import sys
@@ -48,7 +52,8 @@ def main():
     ss = synth.make_streams(nscans, 1, distinct_paths=nscans)
     tot = np.zeros((3, 7))
     segs = np.zeros(3)
-    bal = {(lvl, nw): np.zeros(4) for lvl in range(3) for nw in (4, 2)}
+    bal = {(lvl, nw): np.zeros(4) for lvl in range(3) for nw in (4, 2, 8)}
+    split = np.zeros((3, 2))  # 4 waves, groups split over idle waves: sum of busiest, tiles
     for k in range(nscans):
         pts = ss.points[k, 0, :ss.counts[k, 0]]
         pose = ss.gt[k, 0] * 0  # first scan of each path: pose (0, 0, 0) in its own frame
@@ -103,7 +108,7 @@ def main():
             tot[lvl] += [ntiles, ballot, setup, useful, cone_setup, lanes_setup, lanes_useful]
             segs[lvl] += seg_setup
             # wave balance: per (tile, fan group) the clip setup and the longest walk of its lanes in the tile
-            for th, nw in ((TILE_H, 4), (TILE_H // 2, 2)):
+            for th, nw in ((TILE_H, 4), (TILE_H // 2, 2), (TILE_H * 2, 8)):
                 cost = {}  # tile -> per-wave cost
                 ngroups = {}
                 for i in range(n):
@@ -128,6 +133,16 @@ def main():
                     busy += w.max()
                     mean += w.mean()
                     few += len(d) <= 2
+                    if nw == 4:
+                        # split alternative: a tile crossed by G < 4 groups gives each group 4 // G waves, which split
+                        # its lanes' walks (every wave runs the group's clip setup)
+                        G = len(d)
+                        kk = max(1, 4 // G)
+                        ws = np.zeros(4)
+                        for j, (fi, steps) in enumerate(sorted(d.items())):
+                            for q in range(kk if G < 4 else 1):
+                                ws[(j * kk + q) % 4 if G < 4 else fi % 4] += SETUP + STEP * -(-steps // kk)
+                        split[lvl] += [ws.max(), 1]
                 bal[(lvl, nw)] += np.array([busy, mean, few, len(cost)])
     print(f"{nscans} scans; per scan and level:")
     print("level  box-tiles  ballot-pairs  setups  useful-setups  setups-after-cone  lanes/setup  useful-lanes/setup")
@@ -144,6 +159,21 @@ def main():
         b4, b2 = bal[(lvl, 4)], bal[(lvl, 2)]
         print(f"{lvl:5d} {b4[0] / b4[1]:31.2f} {b4[2] / b4[3]:16.2f} {b4[0] / b4[3]:26.0f}  |  {b2[0] / b2[1]:31.2f} "
               f"{b2[0] / b4[3]:31.0f}")
+    print("8 waves x 64x64 tiles (512-thread workgroups): per level busiest/mean, busiest raster per 64x64 tile, per "
+          "64x32 area, total raster work per 64x32 area vs the 4-wave design's")
+    for lvl in range(3):
+        b4, b8 = bal[(lvl, 4)], bal[(lvl, 8)]
+        print(f"{lvl:5d} {b8[0] / b8[1]:8.2f} {b8[0] / b8[3]:10.0f} {b8[0] / b4[3]:10.0f}   total {8 * b8[1] / b4[3]:8.0f} vs "
+              f"{4 * b4[1] / b4[3]:8.0f}   tiles with steps {b8[3] / nscans:6.0f} vs {b4[3] / nscans:6.0f}")
+    # Wave-slot time: a wave waiting at the tile's barrier holds its slot (registers, LDS) -- with every slot of the
+    # CU taken, the raster's throughput is set by waves x busiest, not by the busiest alone.  This is the reading
+    # the 8-wave build measured (profiles/r06/ab_r06y_update_8waves.md: +33 % slot time here, +26 % update there).
+    print("wave-slot time of the raster per 64x32 area (waves x busiest wave), relative to the 4-wave design:")
+    print("level   4 waves   2 waves x 64x16   8 waves x 64x64   4 waves, groups split over idle waves")
+    for lvl in range(3):
+        b4, b2, b8 = bal[(lvl, 4)], bal[(lvl, 2)], bal[(lvl, 8)]
+        s4 = 4 * b4[0]
+        print(f"{lvl:5d} {s4 / b4[3]:9.0f} {2 * b2[0] / s4:17.2f} {8 * b8[0] / s4:17.2f} {4 * split[lvl][0] / s4:38.2f}")
 
 
 if __name__ == "__main__":

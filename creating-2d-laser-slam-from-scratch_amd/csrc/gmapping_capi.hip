@@ -93,7 +93,7 @@ int launch(gm_ctx *c, int begin, int count, const double *d_poses, const float *
         GCHK(hipEventRecord(ev.first, s));
     }
     hipLaunchKernelGGL(gm_score_kernel, dim3(count), dim3(GM_THREADS), 0, s, c->geom, d_poses, d_ranges, n, c->d_cos,
-                       c->d_sin, c->d_maps, c->d_stamps, c->d_state, d_scores, begin, c->d_rays, c->d_hitxy);
+                       c->d_sin, c->d_maps, c->d_stamps, c->d_state, d_scores, begin, c->d_rays, c->d_hitxy, c->d_hits);
     GCHK(hipGetLastError());
     hipLaunchKernelGGL(gm_compute_kernel, dim3(count * c->parts), dim3(GM_THREADS), gm_shmem(n), s, c->geom, d_poses,
                        n, c->d_rays, c->d_hitxy, c->d_maps, c->d_stamps, c->d_hits, c->d_state, begin, count, c->parts);
@@ -312,6 +312,7 @@ int gm_get_particle_map(gm_ctx *c, int p, int32_t *n_out, int32_t *visits_out, f
         GCHK(hipMemcpy(hits.data(), c->d_hits + (size_t)p * c->max_beams, sizeof(GmHitCell) * st.hit_cells,
                        hipMemcpyDeviceToHost));
         for (const auto &h : hits) {
+            if (h.cell < 0) continue;  // a beam that is not its cell's first hit (or no hit)
             acc_out[2 * (size_t)h.cell] = h.ax;
             acc_out[2 * (size_t)h.cell + 1] = h.ay;
         }

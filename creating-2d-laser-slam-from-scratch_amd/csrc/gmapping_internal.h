@@ -49,7 +49,7 @@ struct alignas(16) GmState {
     int hits;                // hit beams (d < max_urange) of this scan
     long long free_updates;  // Σ (num_points - 1): the free-cell visit updates of this scan
     int step;                // ComputeMap calls so far: tiles stamped `step` belong to the current map
-    int hit_cells;           // entries of the particle's hit-cell list
+    int hit_cells;           // slots of the particle's hit-cell list (one per beam; cell < 0: no entry)
     int pad_[2];
 };
 

@@ -47,6 +47,15 @@ __device__ __forceinline__ void gm_lds_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+#ifndef GM_BALLOT
+#define GM_BALLOT 1  // fan groups culled per tile by one ballot (lane f tests group f); 0: a scalar box test per group
+#endif
+#ifndef GM_RESTORE
+#define GM_RESTORE 1  // the count array is zeroed by the threads that store it (no clear + barrier per tile); 0: A/B
+#endif
+#ifndef GM_PRICE
+#define GM_PRICE 0  // timing-only pricing builds (wrong maps): 1 no acc pass, 2 no count stores, 3 no walk steps
+#endif
 constexpr int GM_STRIDE = 68;                          // LDS words per tile row (16-B rows)
 constexpr int GM_LDS_WORDS = GM_TILE_H * GM_STRIDE;    // one LDS tile array
 
@@ -154,7 +163,8 @@ __global__ void __launch_bounds__(GM_THREADS)
 gm_score_kernel(GmGeom g, const double *__restrict__ poses, const float *__restrict__ ranges, int n,
                 const double *__restrict__ a_cos, const double *__restrict__ a_sin, const unsigned *__restrict__ maps,
                 const int *__restrict__ stamps, GmState *__restrict__ state, int *__restrict__ scores_out,
-                int particle_begin, unsigned *__restrict__ rays_out, float2 *__restrict__ hitxy_out)
+                int particle_begin, unsigned *__restrict__ rays_out, float2 *__restrict__ hitxy_out,
+                GmHitCell *__restrict__ hit_cells)
 {
     __shared__ int s_red[GM_THREADS / 64][2];
     const int p = particle_begin + blockIdx.x;
@@ -170,8 +180,11 @@ gm_score_kernel(GmGeom g, const double *__restrict__ poses, const float *__restr
     gm_world2map(g, px, py, x0, y0);  // p0 = world2map(lp) (:176-179)
     unsigned *prays = rays_out + (size_t)p * g.max_beams;
     float2 *phxy = hitxy_out + (size_t)p * g.max_beams;
+    GmHitCell *phits = hit_cells + (size_t)p * g.max_beams;
     int score = 0, hits = 0;
     for (int b = tid; b < n; b += GM_THREADS) {
+        // the hit-cell list is indexed by beam: gm_compute_kernel fills the slot of a cell's first hitting beam
+        phits[b].cell = -1;
         const GmBeam e = gm_beam(g, px, py, ct, sn, ranges[b], a_cos[b], a_sin[b]);
         unsigned r = GM_RAY_INVALID;
         // lines longer than 16383 cells are not representable (max_range / delta < 16384)
@@ -212,7 +225,7 @@ gm_score_kernel(GmGeom g, const double *__restrict__ poses, const float *__restr
         st.hits = hc;
         st.step = prev_step + 1;   // tiles stamped with this step form the new map
         st.free_updates = 0;
-        st.hit_cells = 0;
+        st.hit_cells = n;  // slots: one per beam, cell < 0 where no list entry
         if (scores_out) scores_out[blockIdx.x] = sc;
     }
 }
@@ -232,6 +245,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
     int4 *gbox = reinterpret_cast<int4 *>(rays + ((n + 3) & ~3));        // per 64-beam fan group
     __shared__ int s_box[4];
     __shared__ int s_anyf[2];   // per tile parity: "some lane marked a cell"
+    __shared__ int s_anyh[2];   // per tile parity: "some beam ends in the tile" (the acc pass runs)
 
     const int part = blockIdx.x / count;
     const int local = blockIdx.x - part * count;
@@ -276,6 +290,13 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
         }
         if ((tid & 63) == 0) gbox[b0 >> 6] = make_int4(gx0, gy0, gx1, gy1);
     }
+    // first_hit starts empty once: afterwards each hit cell's first beam restores its word in the acc pass; with
+    // GM_RESTORE the counts likewise (the store pass zeroes what it stored), and both tile flags start clear
+    for (int k = tid; k < GM_LDS_WORDS / 4; k += GM_THREADS) {
+        reinterpret_cast<uint4 *>(first_hit)[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        if (GM_RESTORE) reinterpret_cast<uint4 *>(cnt)[k] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (tid < 2) s_anyf[tid] = s_anyh[tid] = 0;
     // the written tile box: the rays' box clamped to the map
     atomicMin(&s_box[0], max(bx0, 0)); atomicMin(&s_box[1], max(by0, 0));
     atomicMax(&s_box[2], min(bx1, g.sx - 1)); atomicMax(&s_box[3], min(by1, g.sy - 1));
@@ -287,43 +308,57 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
     if (tid == 0 && part == 0) {
         st.tx0 = tx0; st.ty0 = ty0; st.tx1 = tx1; st.ty1 = ty1;
     }
-    bool any_tile_marks = false;
+    bool any_tile_marks = false, any_tile_hits = false;
 
     long long nfree = 0;
+    const int ngr = (n + 63) >> 6;                                   // fan groups
+    const int wbeam0 = __builtin_amdgcn_readfirstlane(tid & ~63);    // this wave's first beam
     const int ntx = tx1 - tx0 + 1, ntiles = (tx1 >= tx0) ? ntx * (ty1 - ty0 + 1) : 0;
     int it = 0;
     for (int t = part; t < ntiles; t += parts, ++it) {
         const int tx = tx0 + t % ntx, ty = ty0 + t / ntx;
         const int X0 = tx * GM_TILE, Y0 = ty * GM_TILE_H;
         const int X1 = min(X0 + GM_TILE, g.sx), Y1 = min(Y0 + GM_TILE_H, g.sy);
-        for (int k = tid; k < GM_LDS_WORDS / 4; k += GM_THREADS) {
-            reinterpret_cast<uint4 *>(cnt)[k] = make_uint4(0u, 0u, 0u, 0u);
-            reinterpret_cast<uint4 *>(first_hit)[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        if (!GM_RESTORE) {
+            for (int k = tid; k < GM_LDS_WORDS / 4; k += GM_THREADS)
+                reinterpret_cast<uint4 *>(cnt)[k] = make_uint4(0u, 0u, 0u, 0u);
+            // the flag of this parity was last read two tiles ago, with barriers in between
+            if (tid == 0) s_anyf[it & 1] = s_anyh[it & 1] = 0;
+        } else if (tid == 0) {
+            // the OTHER parity's flags, for the next tile: the previous tile read them after its raster barrier and
+            // before its closing one (a tile without marks read s_anyf == 0, which this rewrites unchanged); this
+            // tile's raster barrier orders the reset before the next tile's raster sets them
+            s_anyf[(it & 1) ^ 1] = s_anyh[(it & 1) ^ 1] = 0;
         }
-        // the flag of this parity was last read two tiles ago, with barriers in between
-        if (tid == 0) s_anyf[it & 1] = 0;
-        gm_lds_barrier();
-        for (int b0 = __builtin_amdgcn_readfirstlane(tid & ~63); b0 < n; b0 += GM_THREADS) {
-            const int4 gb = gbox[b0 >> 6];
-            const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
-            const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
-            if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
+        // the fan groups (64 beams) whose box meets the tile: one ballot, lane f testing group f (groups past the
+        // first 64, scans of > 4096 beams, test their box alone); this wave's groups are f = wave + 4 k
+        unsigned long long fm = 0ull;
+        if (GM_BALLOT) {
+            int ol = tid & 63;  // opaque: the box address is not hoisted into a VGPR held across tiles
+            asm volatile("" : "+v"(ol));
+            const int4 gb = gbox[min(ol, ngr - 1)];
+            fm = __ballot((int)(ol < ngr) & (int)(gb.z >= X0) & (int)(gb.x < X1) & (int)(gb.w >= Y0) & (int)(gb.y < Y1));
+        }
+        if (!GM_RESTORE) gm_lds_barrier();  // the cleared counts (GM_RESTORE: the previous tile's closing barrier)
+        // one fan group's raster in the tile (a lambda: the ballot's groups and the scalar-tested groups past the
+        // first 64 share it)
+        auto raster_group = [&](int b0) {
             const int b = b0 + (tid & 63);
-            if (b >= n) continue;
+            if (b >= n) return;
             const unsigned r = rays[b];
-            if (r == GM_RAY_INVALID) continue;
+            if (r == GM_RAY_INVALID) return;
             const int x1 = x0 + (int)(r & 0xFFFFu) - GM_REL, y1 = y0 + (int)((r >> 16) & 0x7FFFu) - GM_REL;
-            if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) continue;
+            if (max(x0, x1) < X0 || min(x0, x1) >= X1 || max(y0, y1) < Y0 || min(y0, y1) >= Y1) return;
             if ((r & GM_RAY_HIT) && x1 >= X0 && x1 < X1 && y1 >= Y0 && y1 < Y1) {
                 const int c = (y1 - Y0) * GM_STRIDE + (x1 - X0);
                 atomicAdd(&cnt[c], 0x10001u);       // n++, visits++ (map.h:40-44)
                 atomicMin(&first_hit[c], (unsigned)b);
-                any_tile_marks = true;
+                any_tile_marks = any_tile_hits = true;
             }
             const GmLine l = gm_line(x0, y0, x1, y1);
             int lo = l.ilo, hi = l.ihi;
             const bool in = l.x_major ? gm_clip(l, X0, X1, Y0, Y1, lo, hi) : gm_clip(l, Y0, Y1, X0, X1, lo, hi);
-            if (!in) continue;
+            if (!in) return;
             const unsigned two_da = 2u * (unsigned)l.da, two_db = 2u * (unsigned)l.db;
             const unsigned num = two_db * (unsigned)lo + (unsigned)l.da;
             const int q = l.da ? (int)gm_udiv(num, two_da) : 0;
@@ -337,6 +372,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
             // incremental walk with f = 2 da - 1 - rem in [0, 2 da): the minor axis steps when f < 2 db --
             // a subtract with borrow and two selects per step on byte offsets into the count array,
             // four steps per trip
+            if (GM_PRICE == 3) return;
             const int tda = (int)two_da, tdb = (int)two_db;
             const int dab = la * 4, dab2 = dab + l.sb * lb * 4;
             int f = tda - 1 - (int)rem;
@@ -358,27 +394,35 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
             }
 #undef GM_WSTEP
             if (i < steps) atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);
+        };
+        for (unsigned long long gmk = fm & (0x1111111111111111ull << (wbeam0 >> 6)); gmk; gmk &= gmk - 1ull)
+            raster_group(__builtin_ctzll(gmk) << 6);
+        for (int b0 = wbeam0 + (GM_BALLOT ? 64 * 64 : 0); b0 < n; b0 += GM_THREADS) {
+            const int4 gb = gbox[b0 >> 6];
+            const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
+            const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
+            if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
+            raster_group(b0);
         }
         if (__ballot(any_tile_marks) && (tid & 63) == 0) s_anyf[it & 1] = 1;
+        if (__ballot(any_tile_hits) && (tid & 63) == 0) s_anyh[it & 1] = 1;
+        any_tile_hits = false;
         gm_lds_barrier();
         // tiles without any mark are not written: their stale stamp makes them read as fresh
         if (!s_anyf[it & 1]) continue;  // plain LDS accesses, ordered by gm_lds_barrier's memory clobber
         any_tile_marks = false;
         unsigned *tp = pm + (size_t)(ty * g.tiles_x + tx) * GM_TILE_BLOCK_WORDS;
         // acc: the first hitting beam of a cell sums every hit of that cell in beam order (:236-240)
-        for (int b0 = __builtin_amdgcn_readfirstlane(tid & ~63); b0 < n; b0 += GM_THREADS) {
-            const int4 gb = gbox[b0 >> 6];
-            const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
-            const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
-            if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
+        auto acc_group = [&](int b0) {
             const int b = b0 + (tid & 63);
-            if (b >= n) continue;
+            if (b >= n) return;
             const unsigned r = rays[b];
-            if (r == GM_RAY_INVALID || !(r & GM_RAY_HIT)) continue;
+            if (r == GM_RAY_INVALID || !(r & GM_RAY_HIT)) return;
             const int x1 = x0 + (int)(r & 0xFFFFu) - GM_REL, y1 = y0 + (int)((r >> 16) & 0x7FFFu) - GM_REL;
-            if (x1 < X0 || x1 >= X1 || y1 < Y0 || y1 >= Y1) continue;
+            if (x1 < X0 || x1 >= X1 || y1 < Y0 || y1 >= Y1) return;
             const int c = (y1 - Y0) * GM_STRIDE + (x1 - X0);
-            if (first_hit[c] != (unsigned)b) continue;
+            if (first_hit[c] != (unsigned)b) return;
+            first_hit[c] = ~0u;  // restored for the next tile (a later beam of the cell then fails the test too)
             float ax = 0.0f, ay = 0.0f;
             const float2 h0 = phxy[b];
             ax += h0.x;
@@ -397,16 +441,33 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
             hc.cell = y1 * g.sx + x1;
             hc.ax = ax;
             hc.ay = ay;
-            phits[atomicAdd(&st.hit_cells, 1)] = hc;
+            // the slot of the cell's first beam: no list counter (a returning global atomic per hit cell, on one
+            // address per particle, was most of this pass's time)
+            phits[b] = hc;
+        };
+        if (GM_PRICE != 1 && s_anyh[it & 1]) {  // (a tile where no beam ends has no acc pass)
+            for (unsigned long long gmk = fm & (0x1111111111111111ull << (wbeam0 >> 6)); gmk; gmk &= gmk - 1ull)
+                acc_group(__builtin_ctzll(gmk) << 6);
+            for (int b0 = wbeam0 + (GM_BALLOT ? 64 * 64 : 0); b0 < n; b0 += GM_THREADS) {
+                const int4 gb = gbox[b0 >> 6];
+                const int gx0 = __builtin_amdgcn_readfirstlane(gb.x), gy0 = __builtin_amdgcn_readfirstlane(gb.y);
+                const int gx1 = __builtin_amdgcn_readfirstlane(gb.z), gy1 = __builtin_amdgcn_readfirstlane(gb.w);
+                if (gx1 < X0 || gx0 >= X1 || gy1 < Y0 || gy0 >= Y1) continue;
+                acc_group(b0);
+            }
         }
-        // counts: the whole tile (a fresh map: untouched cells written as zero), 16-B stores
-        for (int qi = tid; qi < GM_TILE_CELLS / 4; qi += GM_THREADS) {
+        // GM_RESTORE: the acc pass's count reads (n) precede the zeroing below
+        if (GM_RESTORE && s_anyh[it & 1]) gm_lds_barrier();
+        // counts: the whole tile (a fresh map: untouched cells written as zero), 16-B stores; GM_RESTORE: each
+        // quad zeroed by the thread that stored it
+        for (int qi = tid; qi < (GM_PRICE == 2 ? 0 : GM_TILE_CELLS / 4); qi += GM_THREADS) {
             const int row = qi >> 4, c4 = (qi & 15) << 2;
-            *reinterpret_cast<uint4 *>(&tp[row * GM_TILE + c4]) =
-                *reinterpret_cast<const uint4 *>(&cnt[row * GM_STRIDE + c4]);
+            uint4 *q = reinterpret_cast<uint4 *>(&cnt[row * GM_STRIDE + c4]);
+            *reinterpret_cast<uint4 *>(&tp[row * GM_TILE + c4]) = *q;
+            if (GM_RESTORE) *q = make_uint4(0u, 0u, 0u, 0u);
         }
         if (tid == 0) pstamp[ty * g.tiles_x + tx] = cur_step;
-        gm_lds_barrier();  // the tile's LDS counts are read before the next tile clears them
+        gm_lds_barrier();  // the tile's LDS counts are read (GM_RESTORE: and zeroed) before the next tile's raster
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) nfree += __shfl_xor(nfree, off, 64);

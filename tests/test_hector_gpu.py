@@ -682,11 +682,12 @@ def test_nan_pose_is_out_of_map(gpu):
 
 
 # ----------------------------------------------------------------------------- scan-size edge cases
-@pytest.mark.parametrize("n_beams,levels,size", [(2400, 3, 1024), (16000, 2, 512)])
+@pytest.mark.parametrize("n_beams,levels,size", [(2400, 3, 1024), (6000, 2, 1024), (16000, 2, 512)])
 def test_dense_scans_bitexact(gpu, n_beams, levels, size):
-    """Scans larger than the match kernel's register-resident points (> 1280: the strided loop) and,
-    at 16000 beams, larger than the single-kernel update's LDS budget (the binned update takes
-    over): poses, gate and maps bit-exact vs the oracle."""
+    """Scans larger than the match kernel's register-resident points (> 1280: the strided loop); at 6000
+    beams more than 64 fan groups, so the clip update's groups past the ballot's first 64 take its scalar
+    box-test path; and at 16000 beams, larger than the single-kernel update's LDS budget (the binned update
+    takes over): poses, gate and maps bit-exact vs the oracle."""
     S = synth.make_streams(1, 6, seed=4711, n_beams=n_beams)
     fleet = HectorFleet(1, 0.05, size, (0.5, 0.5), levels, max_points=n_beams)
     ora = O.HectorOracle(0.05, size, (0.5, 0.5), levels, reduce_threads=T_RED)

@@ -53,6 +53,12 @@ __device__ __forceinline__ void gm_lds_barrier()
 #ifndef GM_RESTORE
 #define GM_RESTORE 1  // the count array is zeroed by the threads that store it (no clear + barrier per tile); 0: A/B
 #endif
+#ifndef GM_BWD
+#define GM_BWD 1  // odd lanes walk their steps backwards (neighbouring beams at different radii: fewer lanes per LDS word)
+#endif
+#ifndef GM_FAN
+#define GM_FAN 1  // lane l of a fan group rasters beam 2 (l % 32) + l / 32: each 32-lane half spans the fan (0: A/B)
+#endif
 #ifndef GM_PRICE
 #define GM_PRICE 0  // timing-only pricing builds (wrong maps): 1 no acc pass, 2 no count stores, 3 no walk steps
 #endif
@@ -343,7 +349,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
         // one fan group's raster in the tile (a lambda: the ballot's groups and the scalar-tested groups past the
         // first 64 share it)
         auto raster_group = [&](int b0) {
-            const int b = b0 + (tid & 63);
+            const int b = b0 + (GM_FAN ? 2 * (tid & 31) + ((tid >> 5) & 1) : (tid & 63));
             if (b >= n) return;
             const unsigned r = rays[b];
             if (r == GM_RAY_INVALID) return;
@@ -360,22 +366,29 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
             const bool in = l.x_major ? gm_clip(l, X0, X1, Y0, Y1, lo, hi) : gm_clip(l, Y0, Y1, X0, X1, lo, hi);
             if (!in) return;
             const unsigned two_da = 2u * (unsigned)l.da, two_db = 2u * (unsigned)l.db;
-            const unsigned num = two_db * (unsigned)lo + (unsigned)l.da;
+            // GM_BWD: odd lanes start at hi and walk down to lo (the same cells): near the scan origin the lanes of
+            // a fan then sit at two radii per instruction, so half as many of them add to one LDS word (the
+            // atomics to one address serialise)
+            const bool bwd = GM_BWD && (tid & 1);
+            const int s0 = bwd ? hi : lo;
+            const unsigned num = two_db * (unsigned)s0 + (unsigned)l.da;
             const int q = l.da ? (int)gm_udiv(num, two_da) : 0;
             unsigned rem = num - (unsigned)q * two_da;
             const int la = l.x_major ? 1 : GM_STRIDE, lb = l.x_major ? GM_STRIDE : 1;
             const int A0 = l.x_major ? X0 : Y0, B0 = l.x_major ? Y0 : X0;
-            const int li = (l.as + lo - A0) * la + (l.bs + l.sb * q - B0) * lb;
+            const int li = (l.as + s0 - A0) * la + (l.bs + l.sb * q - B0) * lb;
             const int steps = hi - lo + 1;
             nfree += steps;
             any_tile_marks = true;
             // incremental walk with f = 2 da - 1 - rem in [0, 2 da): the minor axis steps when f < 2 db --
             // a subtract with borrow and two selects per step on byte offsets into the count array,
-            // four steps per trip
+            // four steps per trip.  Backwards the same step with f = rem and the offsets negated: rem drops by
+            // 2 db per step and the minor axis steps back exactly when it borrows (then + 2 da)
             if (GM_PRICE == 3) return;
             const int tda = (int)two_da, tdb = (int)two_db;
-            const int dab = la * 4, dab2 = dab + l.sb * lb * 4;
-            int f = tda - 1 - (int)rem;
+            const int dabf = la * 4, dab2f = dabf + l.sb * lb * 4;
+            const int dab = bwd ? -dabf : dabf, dab2 = bwd ? -dab2f : dab2f;
+            int f = bwd ? (int)rem : tda - 1 - (int)rem;
             char *pc = reinterpret_cast<char *>(cnt) + li * 4;
             int i = 0;
 #define GM_WSTEP                                                                  \

@@ -132,8 +132,8 @@ PATCHES = {
                  "__device__ __forceinline__ void upd_store(int4 *p, int4 v)\n{\n    if (v.x == 1234) *p = v;\n    return;\n#if S2D_NT_STORE"),
                 (K, "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n#if S2D_NT_STORE",
                  "__device__ __forceinline__ void upd_store(int *p, int v)\n{\n    if (v == 1234) *p = v;\n    return;\n#if S2D_NT_STORE")],
-    "noord": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "")],
-    "ordbm": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "                (void)uv;\n"),
+    "noord": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[ou]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[ou + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "")],
+    "ordbm": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[ou]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[ou + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "                (void)uv;\n"),
               (K, "                touched += qb_count(mb);\n            }\n            pend_tl = nullptr;\n",
                "                touched += qb_count(mb);\n            }\n            {\n                unsigned bm = 0u;\n#pragma unroll\n"
                "                for (int j = 0; j < UPD_QUADS; ++j) {\n                    const unsigned u = ~qb[j] & QB_UNMASK;\n"
@@ -142,7 +142,7 @@ PATCHES = {
                "                if (__any(bm != 0u)) {\n                    tu[qtid] = (unsigned short)bm;\n"
                "                    if (lane == 0) *reinterpret_cast<uint4 *>(&pend_tl[ORD_OFF + 512 + 4 * (qtid >> 6)]) = "
                "make_uint4(mark_free, (unsigned)(size_t)pend_tl, 0u, 0u);\n                }\n            }\n            pend_tl = nullptr;\n")],
-    "ordbm2": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "                (void)uv;\n"),
+    "ordbm2": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[ou]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[ou + (unsigned)c] = (unsigned short)uv[c];\n                }\n", "                (void)uv;\n"),
                (K, "                touched += qb_count(mb);\n            }\n            pend_tl = nullptr;\n",
                 "                touched += qb_count(mb);\n            }\n            {\n                unsigned bm = 0u;\n#pragma unroll\n"
                 "                for (int j = 0; j < UPD_QUADS; ++j) {\n                    const unsigned u = ~qb[j] & QB_UNMASK;\n"
@@ -152,8 +152,8 @@ PATCHES = {
     "valu100": [(K, "        const int X0 = tx * TILE, Y0 = ty * UPD_TH;\n",
                  "        const int X0 = tx * TILE, Y0 = ty * UPD_TH;\n"
                  "        { float dmy_; asm volatile(\".rept 100\\n\\tv_add_f32 %0, %1, %2\\n\\t.endr\" : \"=v\"(dmy_) : \"v\"((float)X0), \"v\"((float)Y0)); }\n")],
-    "ordfull": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[o + (unsigned)c] = (unsigned short)uv[c];\n                }\n",
-                 "                *reinterpret_cast<uint2 *>(&tu[o]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n")],
+    "ordfull": [(K, "                if (qb_all(mb)) {\n                    *reinterpret_cast<uint2 *>(&tu[ou]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n                } else {\n#pragma unroll\n                    for (int c = 0; c < 4; ++c)\n                        if (qb_cell(mb, c)) tu[ou + (unsigned)c] = (unsigned short)uv[c];\n                }\n",
+                 "                *reinterpret_cast<uint2 *>(&tu[ou]) = make_uint2(uv[0] | (uv[1] << 16), uv[2] | (uv[3] << 16));\n")],
     "uclk": [(K, "    for (int ii = 0; ii <= my_tiles; ++ii) {\n        const int i = __builtin_amdgcn_readfirstlane(ii);  // uniform (the compiler had put it in a VGPR)\n        const int qtid = tid;",
               "    unsigned long long u_r = 0, u_w = 0, u_a = 0, u_b = 0, u_m = 0, u_t = __builtin_amdgcn_s_memtime();\n"
               "#define UCLK(acc) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); acc += t_ - u_t; u_t = t_; } while (0)\n"

@@ -143,6 +143,26 @@ def test_beams_leaving_the_map_and_empty_scan(gpu):
         assert v.sum() == 0 and n.sum() == 0
 
 
+@pytest.mark.parametrize("n_beams", [2400, 6000])
+def test_dense_scans(gpu, n_beams):
+    """Scans of more beams than the default 1081: at 2400 the hit-cell slots and the ballot over 38 fan groups;
+    at 6000, 94 fan groups, so gm_compute_kernel's groups past the ballot's first 64 take the scalar box-test
+    path (raster and acc pass).  Counts, accumulators and publish bit-exact vs the oracle, two steps."""
+    ang = synth.beam_angles(n_beams).astype(np.float64)
+    segs = synth.world_segments()
+    gt = synth.trajectory(2, 0.0)
+    P = 3
+    fleet = GMappingFleet(P, max_beams=n_beams)
+    fleet.set_beams(ang)
+    rng = np.random.default_rng(n_beams)
+    for t in range(2):
+        ranges = synth.cast_ranges(gt[t:t + 1], segs, n_beams)[0].astype(np.float32)
+        ranges += rng.normal(0, 0.01, ranges.shape).astype(np.float32)
+        poses4 = GMappingFleet.poses4(gt[t] + rng.normal(0, [0.05, 0.05, 0.02], size=(P, 3)))
+        fleet.compute(poses4, ranges)
+        _check_maps(fleet, _oracle_maps(poses4, ranges, ang), P)
+
+
 def test_device_entry_and_scores_buffer(gpu):
     import torch
 

@@ -61,6 +61,7 @@ round-3 clip kernel (run them with SLAM2D_UPD_KERNEL=clip).
   mclk       same results   hs_match_kernel's chain wave sums s_memtime cycles per Gauss-Newton step: step start -> chain
                             start (gathers, conversions, chunk 0), the chain, its end -> the next step (solve, broadcast);
                             tools/clk_match.py reads them
+  mclkbar    same results   mclk, with stamp 3 = the chain wave's cycles inside its chunk barriers (chunks 1..)
   cheapprob  WRONG RESULTS  cell_prob is one multiply-add instead of exp + division (prices the match's probability
                             conversions: their VALU and their place on the per-stream path)
   mlds4      same results   hs_match_kernel with 1.2 KB of unused LDS (5 -> 4 workgroups per CU: is the chain's
@@ -196,10 +197,31 @@ PATCHES = {
               "    if (threadIdx.x < 8) s_mk[threadIdx.x] = 0ull;\n    load_exptab();\n    if (!fused) __syncthreads();"),
              (K, "    clk_stamp(geom.clk, 0, false);\n    if (threadIdx.x != 0) return;",
               "    clk_stamp(geom.clk, 0, false);\n    if (threadIdx.x == 0) for (int k = 0; k < 8; ++k) atomicAdd(&g_stamps[k], s_mk[k]);\n    if (threadIdx.x != 0) return;")],
+    # mclk with stamp 3 = the chain wave's cycles inside its chunk barriers (chunks 1..), instead of the count of
+    # steps with >= 512 misses (tools/clk_match.py with CLK_BAR=1)
+    "mclkbar": None,
     "cheapprob": [(K, "    float odds = sdm_expf_tab(l, s_exptab);\n    return __fdiv_rn(odds, odds + 1.0f);",
                    "    return l * 0.25f + 0.5f;")],
     "ktnoswar": [("karto_kernels.hip", "    return b ^ ((a ^ b) & (t - (t >> 7)));", "    return b | (t & 0u);")],
 }
+
+
+def _mclkbar():
+    out = []
+    for fname, a, b in PATCHES["mclk"]:
+        if "mk_big = tot >= 512;" in b:
+            b = b.replace("        if (tid == 0 && mk_big) s_mk[3] += 1ull;\n", "")
+        out.append((fname, a, b))
+    out.append((K, "            if (CW_BUFS == 1 && (!CW_SHARE || j > 0)) lds_barrier();\n            lds_barrier();\n"
+                   "            if (j == 0) mk_t1 = __builtin_amdgcn_s_memtime();\n",
+                "            const unsigned long long mk_b0 = __builtin_amdgcn_s_memtime();\n"
+                "            if (CW_BUFS == 1 && (!CW_SHARE || j > 0)) lds_barrier();\n            lds_barrier();\n"
+                "            if (j == 0) mk_t1 = __builtin_amdgcn_s_memtime();\n"
+                "            else if (lane == 0) s_mk[3] += __builtin_amdgcn_s_memtime() - mk_b0;\n"))
+    return out
+
+
+PATCHES["mclkbar"] = _mclkbar()
 
 
 def build(variant: str) -> str:
@@ -229,11 +251,15 @@ def check() -> list:
     """Variants whose patch anchors no longer occur exactly once in the sources (tests/test_host_cpu.py)."""
     bad = []
     for v, patches in sorted(PATCHES.items()):
-        for fname, old, _ in patches:
-            with open(os.path.join(PKG, "csrc", fname)) as f:
-                if f.read().count(old) != 1:
-                    bad.append(v)
-                    break
+        text = {}  # the variant's patches apply in order, each to the text the previous ones left (as build() does)
+        for fname, old, new in patches:
+            if fname not in text:
+                with open(os.path.join(PKG, "csrc", fname)) as f:
+                    text[fname] = f.read()
+            if text[fname].count(old) != 1:
+                bad.append(v)
+                break
+            text[fname] = text[fname].replace(old, new)
     return bad
 
 

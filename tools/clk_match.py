@@ -47,6 +47,9 @@ print(f"chain cycles per term: {st[1] / n / 1081:.2f}")
 for name, v in (("point wave: transform + gathers + parking", st[4]), ("point wave: shared conversion", st[5]),
                 ("point wave: chunk 0 terms", st[6])):
     print(f"{name:55s} {v / n:9.0f} cycles per GN step")
-print(f"steps with >= 512 misses: {nbig} ({nbig / n:.3f} of all); their shared conversion {st[7] / nbig:.0f} cycles, "
-      f"the other steps' {(st[5] - st[7]) / max(n - nbig, 1):.0f}")
+if os.environ.get("CLK_BAR") == "1":  # the mclkbar build: stamp 3 = chain-wave cycles inside chunk barriers
+    print(f"{'chain: inside its chunk barriers (chunks 1..)':55s} {st[3] / n:9.0f} cycles per GN step")
+else:
+    print(f"steps with >= 512 misses: {nbig} ({nbig / n:.3f} of all); their shared conversion {st[7] / nbig:.0f} cycles, "
+          f"the other steps' {(st[5] - st[7]) / max(n - nbig, 1):.0f}")
 fleet.close()

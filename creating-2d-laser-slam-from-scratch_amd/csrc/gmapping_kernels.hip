@@ -5,7 +5,14 @@
 //   gm_compute_kernel   `parts` 256-thread workgroups per particle: GMapping::ComputeMap
 //                       (lesson4/src/gmapping/gmapping.cc:171-242) of the shared scan seen from the
 //                       particle's pose, into the particle's tiled packed-count map (part q draws
-//                       tiles q, q + parts, ...) and its list of hit cells with their accumulators.
+//                       tiles q, q + parts, ...) and its hit-cell slots (one per beam: the slot of a
+//                       cell's first hitting beam carries the cell and its accumulators).
+//
+// Per tile (round 6, the Hector update's idioms): one ballot picks the fan groups whose box meets the tile;
+// the raster marks counts (and first-hit words) in LDS; an acc pass runs only when some beam ends in the tile;
+// the counts are stored whole (a fresh map) by threads that zero the words they stored, so a tile needs
+// no clear; first-hit words are restored by each hit cell's first beam.  Odd lanes walk backwards and each
+// 32-lane half of a wave spans its 64-beam fan, spreading the LDS atomics near the scan origin.
 //
 // Raster: GridLineTraversal::gridLine (lesson4/include/lesson4/gmapping/grid/gridlinetraversal.h:
 // 27-207) starts at the endpoint with the smaller major coordinate and, with decision variable

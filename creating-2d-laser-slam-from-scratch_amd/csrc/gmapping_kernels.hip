@@ -67,7 +67,8 @@ __device__ __forceinline__ void gm_lds_barrier()
 #define GM_FAN 1  // lane l of a fan group rasters beam 2 (l % 32) + l / 32: each 32-lane half spans the fan (0: A/B)
 #endif
 #ifndef GM_PRICE
-#define GM_PRICE 0  // timing-only pricing builds (wrong maps): 1 no acc pass, 2 no count stores, 3 no walk steps
+#define GM_PRICE 0  // timing-only pricing builds (wrong maps): 1 no acc pass, 2 no count stores (invalid with
+                    // GM_RESTORE: the counts then pile up), 3 no walk steps
 #endif
 constexpr int GM_STRIDE = 68;                          // LDS words per tile row (16-B rows)
 constexpr int GM_LDS_WORDS = GM_TILE_H * GM_STRIDE;    // one LDS tile array

@@ -66,10 +66,17 @@ __device__ __forceinline__ void gm_lds_barrier()
 #ifndef GM_FAN
 #define GM_FAN 1  // lane l of a fan group rasters beam 2 (l % 32) + l / 32: each 32-lane half spans the fan (0: A/B)
 #endif
+#ifndef GM_PACKED
+#define GM_PACKED 1  // the walk's error term and LDS address packed in one register, eight steps per trip (0: A/B)
+#endif
 #ifndef GM_PRICE
 #define GM_PRICE 0  // timing-only pricing builds (wrong maps): 1 no acc pass, 2 no count stores (invalid with
                     // GM_RESTORE: the counts then pile up), 3 no walk steps
 #endif
+// 32-bit LDS byte address of an LDS pointer, and back (GM_PACKED carries addresses in packed registers)
+typedef __attribute__((address_space(3))) unsigned gm_lds_u32;
+__device__ __forceinline__ unsigned gm_lds_addr(unsigned *p) { return (unsigned)(size_t)(gm_lds_u32 *)p; }
+__device__ __forceinline__ unsigned *gm_lds_ptr(unsigned a) { return (unsigned *)(gm_lds_u32 *)(size_t)a; }
 constexpr int GM_STRIDE = 68;                          // LDS words per tile row (16-B rows)
 constexpr int GM_LDS_WORDS = GM_TILE_H * GM_STRIDE;    // one LDS tile array
 
@@ -397,8 +404,36 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
             const int dabf = la * 4, dab2f = dabf + l.sb * lb * 4;
             const int dab = bwd ? -dabf : dabf, dab2 = bwd ? -dab2f : dab2f;
             int f = bwd ? (int)rem : tda - 1 - (int)rem;
-            char *pc = reinterpret_cast<char *>(cnt) + li * 4;
             int i = 0;
+#if GM_PACKED
+            // f and the step's LDS byte address in ONE register, V = f << 16 | address (LDS addresses < 2^16, f < 2 da
+            // <= 2^15): subtracting 2 db << 16 borrows exactly when the minor axis steps, and one select + add then
+            // moves both fields (the Hector update's walk); eight steps per trip
+            const unsigned vdn = (unsigned)tdb << 16;
+            const unsigned vk_major = (unsigned)dab, vk_minor = ((unsigned)tda << 16) + (unsigned)dab2;
+            unsigned v = ((unsigned)f << 16) + gm_lds_addr(cnt) + (unsigned)li * 4u;
+#define GM_WSTEP                                                                   \
+    do {                                                                           \
+        atomicAdd(gm_lds_ptr(v & 0xFFFFu), 1u); /* visits++ (:227-234) */          \
+        unsigned vn_;                                                              \
+        const bool c_ = __builtin_sub_overflow(v, vdn, &vn_);                      \
+        v = vn_ + (c_ ? vk_minor : vk_major);                                      \
+    } while (0)
+            for (; i + 7 < steps; i += 8) {
+                GM_WSTEP; GM_WSTEP; GM_WSTEP; GM_WSTEP; GM_WSTEP; GM_WSTEP; GM_WSTEP; GM_WSTEP;
+            }
+            if (i + 3 < steps) {
+                GM_WSTEP; GM_WSTEP; GM_WSTEP; GM_WSTEP;
+                i += 4;
+            }
+            if (i + 1 < steps) {
+                GM_WSTEP; GM_WSTEP;
+                i += 2;
+            }
+#undef GM_WSTEP
+            if (i < steps) atomicAdd(gm_lds_ptr(v & 0xFFFFu), 1u);
+#else
+            char *pc = reinterpret_cast<char *>(cnt) + li * 4;
 #define GM_WSTEP                                                                  \
     do {                                                                          \
         atomicAdd(reinterpret_cast<unsigned *>(pc), 1u); /* visits++ (:227-234) */ \
@@ -415,6 +450,7 @@ gm_compute_kernel(GmGeom g, const double *__restrict__ poses, int n, const unsig
             }
 #undef GM_WSTEP
             if (i < steps) atomicAdd(reinterpret_cast<unsigned *>(pc), 1u);
+#endif
         };
         for (unsigned long long gmk = fm & (0x1111111111111111ull << (wbeam0 >> 6)); gmk; gmk &= gmk - 1ull)
             raster_group(__builtin_ctzll(gmk) << 6);

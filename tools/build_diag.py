@@ -86,7 +86,7 @@ PATCHES = {
     "hwexp": [(K, "    float odds = sdm_expf_tab(l, s_exptab);", "    float odds = __expf(l);")],
     "gmplain": [("gmapping_kernels.hip", "        atomicAdd(reinterpret_cast<unsigned *>(pc), 1u); /* visits++ (:227-234) */ \\\n",
                  "        *reinterpret_cast<volatile unsigned *>(pc) = 1u;                             \\\n")],
-    "gmnowalk": [("gmapping_kernels.hip", "            int i = 0;\n#define GM_WSTEP", "            int i = steps;\n#define GM_WSTEP")],
+    "gmnowalk": [("gmapping_kernels.hip", "            if (GM_PRICE == 3) return;\n", "            return;\n")],  # (= GM_PRICE=3)
     "plfastatan": [("plicp_kernels.hip", '#include "detmath.h"\n',
                     '#include "detmath.h"\n#define sdm_atan2(y, x) ((double)atan2f((float)(y), (float)(x)))\n'
                     '#define sdm_atan(x) ((double)atanf((float)(x)))\n')],
